@@ -1,0 +1,57 @@
+"""Shared test helpers: golden fixtures, seeded weights, object-config flags."""
+import json
+import os
+
+import numpy as np
+import torch
+
+from recipe import MODEL_CASES, case_by_name, seeded_state_dict, seeded_input  # noqa: F401
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+_MODELS = None
+
+
+def models_index():
+    global _MODELS
+    if _MODELS is None:
+        with open(os.path.join(GOLDEN, "models.json")) as f:
+            _MODELS = json.load(f)
+    return _MODELS
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name if name.endswith(".npz") else name + ".npz"))
+
+
+def case_flags(case):
+    o = case["objects"]
+    return dict(keypoints=o.get("keypoints_per_label", 0) > 0, yaw=o.get("yaw", False),
+                pitch=o.get("pitch", False), roll=o.get("roll", False), depth=o.get("depth", False))
+
+
+def case_state_dict(name):
+    """Seeded weights for a model case, checked against the checksums the reference run stored."""
+    entry = models_index()[name]
+    sd = seeded_state_dict([(k, s) for k, s in entry["keys"]])
+    checks = golden(f"model_{name}")["weight_checksums"]
+    got = np.array([[float(v.double().sum()), float(v.double().abs().sum())]
+                    if v.dtype.is_floating_point else [float(v), 0.0] for v in sd.values()])
+    assert np.array_equal(got, checks), "seeded weight recipe drifted from the golden run"
+    return sd
+
+
+def case_input(name):
+    case = case_by_name(name)
+    img = seeded_input(case)
+    chk = golden(f"model_{name}")["img_checksum"]
+    assert float(img.double().sum()) == chk[0] and float(img.double().abs().sum()) == chk[1]
+    return img
+
+
+def keypoint_owner(case):
+    o = case["objects"]
+    owner = []
+    for lab in range(o["n_labels"]):
+        for slot in range(o.get("keypoints_per_label", 0)):
+            owner.append((lab, slot))
+    return owner

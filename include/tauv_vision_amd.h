@@ -1,0 +1,130 @@
+/*
+ * tauv-vision_amd — C ABI of the MI355X (gfx950) CenterNet detection hot path.
+ *
+ * Drop-in boundary for TAUV-Vision's per-frame CenterNet path (reference
+ * Tartan-AUV/TAUV-Vision @ 2024_10_08). The reference is pure Python on PyTorch; each
+ * entry point below replaces the reference interface cited next to it. Plain pointers
+ * and sizes only (device pointers are HIP device addresses, e.g. a torch tensor's
+ * data_ptr()); `stream` is a hipStream_t (NULL = default stream). No exceptions cross
+ * this ABI: every call returns TV_OK or a TV_E* code and sets a thread-local message
+ * readable with tv_last_error().
+ *
+ * Layouts
+ *   image input   fp32 NCHW [B,3,in_h,in_w], ImageNet-normalised (Centernet.forward,
+ *                 centernet.py:65) — or raw u8 frames NHWC [B,in_h,in_w,3] with the
+ *                 node's ToTensor+Normalize fused (centernet_node.py:90-92).
+ *   head output   fp32 NHWC [B,out_h,out_w,out_cpad]; channel order = the reference
+ *                 get_head_channels() order (centernet.py:114-142), out_cpad = round
+ *                 up of the channel total to 4. Prediction fields are channel slices.
+ *   records       fp32 [B][K][10] = label, score, y, x, h, w, depth (NaN if absent),
+ *                 flat peak index (label*H*W + y*W + x), aux0, aux1 (optional pair
+ *                 gathered at (label, y, x), e.g. the keypoint affinity of
+ *                 decode.py:121-122; NaN if absent); counts int32 [B] = number of
+ *                 records with score >= threshold (the host loop's break, decode.py:207).
+ */
+#ifndef TAUV_VISION_AMD_H
+#define TAUV_VISION_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TV_OK 0
+#define TV_EINVAL 1    /* bad argument (maps to ValueError / AssertionError) */
+#define TV_ESHAPE 2    /* shape the reference would also reject */
+#define TV_EHIP 3      /* HIP runtime error */
+#define TV_ENOTFOUND 4 /* missing state_dict key */
+#define TV_ENOMEM 5
+
+typedef enum tv_dtype { TV_F32 = 0, TV_F16 = 1, TV_BF16 = 2 } tv_dtype;
+
+/* Model description: the fields of ModelConfig (config.py:6-35) plus the head list of
+ * get_head_channels() (centernet.py:114-142). */
+typedef struct tv_model_desc {
+  int32_t n_levels;          /* len(backbone_heights) */
+  int32_t heights[8];        /* backbone_heights */
+  int32_t channels[9];       /* backbone_channels, n_levels + 1 entries */
+  int32_t downsamples;       /* ModelConfig.downsamples */
+  int32_t n_heads;
+  int32_t head_channels[16]; /* get_head_channels(object_config) */
+  int32_t in_h, in_w;        /* ModelConfig.in_h / in_w */
+  int32_t compute_dtype;     /* tv_dtype: TV_F32 = exact-f32 parity mode */
+} tv_model_desc;
+
+typedef struct tv_engine tv_engine;
+
+typedef struct tv_weight_view {
+  const char* name;  /* reference state_dict key, e.g. "backbone.dla_down.projection_layer.0.weight" */
+  const float* data; /* host fp32, contiguous, PyTorch layout */
+  int64_t numel;
+} tv_weight_view;
+
+/* Reference state_dict layout of Centernet(DLABackbone(...)) in registration order
+ * (what nn.Module.state_dict() yields; replaces model.state_dict() key/shape discovery,
+ * centernet.py:32-61, dla.py:8-416). num_batches_tracked entries have ndim 0. */
+int tv_model_param_count(const tv_model_desc* desc, int32_t* count);
+int tv_model_param_info(const tv_model_desc* desc, int32_t index, char* name, int32_t name_cap,
+                        int64_t shape[4], int32_t* ndim);
+/* Algorithmic FLOPs per frame (2*MAC over every conv / conv-transpose) and output geometry. */
+int tv_model_geometry(const tv_model_desc* desc, double* flops_per_frame, int32_t* out_h, int32_t* out_w,
+                      int32_t* out_channels, int32_t* out_cpad);
+
+/* Build an engine from reference-layout weights (replaces Centernet(...).to(device) +
+ * load_state_dict(torch.load(...)) + eval(), centernet_node.py:46-48). BatchNorm is
+ * folded (eval semantics, eps 1e-5); the engine owns its device copy and is immutable
+ * after create, so concurrent forwards on different streams are safe. */
+int tv_engine_create(const tv_model_desc* desc, const tv_weight_view* weights, int32_t n_weights,
+                     int32_t device, tv_engine** out);
+int tv_engine_destroy(tv_engine* engine);
+/* Allocate the per-(stream, batch) workspace up front (required before graph capture). */
+int tv_engine_prepare(tv_engine* engine, int32_t batch, void* stream);
+/* Centernet.forward(img) -> Prediction heads (centernet.py:65-92). Async on `stream`. */
+int tv_engine_forward(tv_engine* engine, const float* img_nchw, int32_t batch, float* out_nhwc, void* stream);
+/* Same from raw u8 RGB frames with ToTensor + Normalize fused (centernet_node.py:90-92). */
+int tv_engine_forward_u8(tv_engine* engine, const uint8_t* frames_nhwc, int32_t batch, float* out_nhwc,
+                         void* stream);
+/* Per-launch timing of one forward (HIP events on `stream`, synchronous): ms[i], flops[i]
+ * per launch i < *n_ops (cap entries max); label(i) describes launch i. */
+int tv_engine_profile(tv_engine* engine, const float* img_nchw, int32_t batch, float* out_nhwc, void* stream,
+                      float* ms, double* flops, int32_t cap, int32_t* n_ops);
+const char* tv_engine_op_label(tv_engine* engine, int32_t index);
+
+/* heatmap_nms(sigmoid?(heat), k) (decode.py:239-252) over any strided [B,C,H,W] fp32
+ * view; `out` is dense [B,C,H,W]. k must be odd and >= 1 (else TV_EINVAL, like the
+ * reference's assert). */
+int tv_heatmap_nms(const float* heat, const int64_t strides[4], int32_t B, int32_t C, int32_t H, int32_t W,
+                   int32_t kernel_size, int32_t apply_sigmoid, float* out, void* stream);
+/* heatmap_detect (decode.py:255-279) on a dense [B, n] map: exact top-K per row,
+ * descending, ties to the smaller flat index. */
+int tv_heatmap_topk(const float* peaks, int32_t B, int64_t n, int32_t K, float* score, int32_t* index,
+                    void* stream);
+/* heatmap_detect()'s index [B,K,2] (y, x) and label [B,K] (int64) from flat indices
+ * (decode.py:271-277; integer division, identical to the reference's float32 division
+ * while C*H*W < 2^24). */
+int tv_index_split(const int32_t* flat, int32_t B, int32_t K, int32_t H, int32_t W, int64_t* index, int64_t* label,
+                   void* stream);
+/* decode() (decode.py:179-236) / the object and keypoint parts of decode_keypoints()
+ * (decode.py:56-135).
+ * mode 0: y = (R*iy + offset_y)/in_h, depth = 1/sigmoid(d) - 1; mode 1: y = iy/out_h,
+ * depth = 1/sigmoid(d), offset unused. Strides are element strides of the [B,C,H,W]
+ * heatmap view and of the [B,H,W,ch] size/offset/depth views (depth may be NULL).
+ * aux (may be NULL): pair gathered per record at element (b, label, j, y, x) with
+ * aux_strides[5] (the [B,K,2,H,W] keypoint_affinity view).
+ * workspace: tv_decode_workspace_size() bytes of device memory. */
+int tv_decode_workspace_size(int32_t B, int32_t C, int32_t H, int32_t W, int32_t K, int64_t* bytes);
+int tv_decode(const float* heat, const int64_t heat_strides[4], const float* size, const int64_t size_strides[4],
+              const float* offset, const int64_t offset_strides[4], const float* depth,
+              const int64_t depth_strides[4], int32_t B, int32_t C, int32_t H, int32_t W, int32_t K,
+              int32_t mode, int32_t ratio, int32_t in_h, int32_t in_w, float score_threshold,
+              const float* aux, const int64_t aux_strides[5], float* records, int32_t* counts, void* workspace,
+              int64_t workspace_bytes, void* stream);
+
+const char* tv_last_error(void);
+const char* tv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,218 @@
+// extern "C" boundary (include/tauv_vision_amd.h). No exceptions cross it.
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "engine.h"
+
+namespace tv {
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+}  // namespace tv
+
+using namespace tv;
+
+#define TV_GUARD(body)                                     \
+  try {                                                    \
+    body                                                   \
+  } catch (const std::bad_alloc&) {                        \
+    set_error("host allocation failed");                   \
+    return TV_ENOMEM;                                      \
+  } catch (const std::exception& e) {                      \
+    set_error(e.what());                                   \
+    return TV_EINVAL;                                      \
+  } catch (...) {                                          \
+    set_error("unknown C++ exception");                    \
+    return TV_EINVAL;                                      \
+  }
+
+struct tv_engine {
+  Engine e;
+};
+
+extern "C" {
+
+const char* tv_last_error(void) { return g_err.c_str(); }
+const char* tv_version(void) { return "tauv-vision_amd 0.1 (gfx950)"; }
+
+int tv_model_param_count(const tv_model_desc* d, int32_t* count) {
+  TV_GUARD({
+    if (!d || !count) { set_error("null argument"); return TV_EINVAL; }
+    Plan p;
+    int rc = build_plan(*d, &p);
+    if (rc) return rc;
+    *count = (int32_t)p.params.size();
+    return TV_OK;
+  })
+}
+
+int tv_model_param_info(const tv_model_desc* d, int32_t i, char* name, int32_t cap, int64_t shape[4], int32_t* ndim) {
+  TV_GUARD({
+    if (!d || !name || !shape || !ndim) { set_error("null argument"); return TV_EINVAL; }
+    Plan p;
+    int rc = build_plan(*d, &p);
+    if (rc) return rc;
+    if (i < 0 || i >= (int)p.params.size()) { set_error("param index out of range"); return TV_EINVAL; }
+    const ParamInfo& pi = p.params[i];
+    if ((int)pi.name.size() + 1 > cap) { set_error("name buffer too small"); return TV_EINVAL; }
+    std::memcpy(name, pi.name.c_str(), pi.name.size() + 1);
+    *ndim = (int32_t)pi.shape.size();
+    for (size_t k = 0; k < 4; ++k) shape[k] = k < pi.shape.size() ? pi.shape[k] : 0;
+    return TV_OK;
+  })
+}
+
+int tv_model_geometry(const tv_model_desc* d, double* flops, int32_t* oh, int32_t* ow, int32_t* oc, int32_t* ocp) {
+  TV_GUARD({
+    if (!d) { set_error("null argument"); return TV_EINVAL; }
+    Plan p;
+    int rc = build_plan(*d, &p);
+    if (rc) return rc;
+    if (flops) *flops = p.flops_per_frame;
+    if (oh) *oh = p.out_h;
+    if (ow) *ow = p.out_w;
+    if (oc) *oc = p.out_c;
+    if (ocp) *ocp = p.out_cpad;
+    return TV_OK;
+  })
+}
+
+int tv_engine_create(const tv_model_desc* d, const tv_weight_view* w, int32_t n, int32_t device, tv_engine** out) {
+  TV_GUARD({
+    if (!d || !out || (n && !w)) { set_error("null argument"); return TV_EINVAL; }
+    tv_engine* e = new tv_engine();
+    int rc = e->e.create(*d, w, n, device);
+    if (rc) {
+      delete e;
+      return rc;
+    }
+    *out = e;
+    return TV_OK;
+  })
+}
+
+int tv_engine_destroy(tv_engine* e) {
+  TV_GUARD({
+    delete e;
+    return TV_OK;
+  })
+}
+
+int tv_engine_prepare(tv_engine* e, int32_t B, void* stream) {
+  TV_GUARD({
+    if (!e || B < 1) { set_error("bad argument"); return TV_EINVAL; }
+    Workspace* ws;
+    return e->e.get_workspace(B, (hipStream_t)stream, &ws);
+  })
+}
+
+int tv_engine_forward(tv_engine* e, const float* img, int32_t B, float* out, void* stream) {
+  TV_GUARD({
+    if (!e) { set_error("null engine"); return TV_EINVAL; }
+    return e->e.forward(img, 0, B, out, (hipStream_t)stream);
+  })
+}
+
+int tv_engine_forward_u8(tv_engine* e, const uint8_t* frames, int32_t B, float* out, void* stream) {
+  TV_GUARD({
+    if (!e) { set_error("null engine"); return TV_EINVAL; }
+    return e->e.forward(frames, 1, B, out, (hipStream_t)stream);
+  })
+}
+
+int tv_engine_profile(tv_engine* e, const float* img, int32_t B, float* out, void* stream, float* ms, double* flops,
+                      int32_t cap, int32_t* n_ops) {
+  TV_GUARD({
+    if (!e || !ms || !flops || !n_ops) { set_error("null argument"); return TV_EINVAL; }
+    int n = 0;
+    int rc = e->e.profile(img, B, out, (hipStream_t)stream, ms, flops, cap, &n);
+    *n_ops = n;
+    return rc;
+  })
+}
+
+const char* tv_engine_op_label(tv_engine* e, int32_t i) {
+  if (!e || i < 0 || i >= (int)e->e.plan.ops.size()) return "";
+  return e->e.plan.ops[i].label.c_str();
+}
+
+int tv_heatmap_nms(const float* heat, const int64_t st[4], int32_t B, int32_t C, int32_t H, int32_t W, int32_t k,
+                   int32_t apply_sigmoid, float* out, void* stream) {
+  TV_GUARD({
+    if (k < 1 || k % 2 == 0) { set_error("kernel_size must be odd and >= 1"); return TV_EINVAL; }
+    if (!heat || !st || !out || B < 0 || C < 0 || H < 0 || W < 0) { set_error("bad argument"); return TV_EINVAL; }
+    return launch_peaks(heat, st, B, C, H, W, k, apply_sigmoid, out, (hipStream_t)stream);
+  })
+}
+
+int tv_heatmap_topk(const float* peaks, int32_t B, int64_t n, int32_t K, float* score, int32_t* index, void* stream) {
+  TV_GUARD({
+    if (!peaks || !score || !index || B < 1) { set_error("bad argument"); return TV_EINVAL; }
+    return launch_topk(peaks, B, n, K, score, index, (hipStream_t)stream);
+  })
+}
+
+int tv_index_split(const int32_t* flat, int32_t B, int32_t K, int32_t H, int32_t W, int64_t* index, int64_t* label,
+                   void* stream) {
+  TV_GUARD({
+    if (!flat || !index || !label || B < 0 || K < 0 || H < 1 || W < 1) { set_error("bad argument"); return TV_EINVAL; }
+    return launch_index_split(flat, B, K, H, W, index, label, (hipStream_t)stream);
+  })
+}
+
+int tv_decode_workspace_size(int32_t B, int32_t C, int32_t H, int32_t W, int32_t K, int64_t* bytes) {
+  if (!bytes || B < 1 || C < 1 || H < 1 || W < 1 || K < 1) { set_error("bad argument"); return TV_EINVAL; }
+  int64_t peaks = ((int64_t)B * C * H * W * 4 + 255) / 256 * 256;
+  int64_t sel = ((int64_t)B * K * 8 + 255) / 256 * 256;
+  *bytes = peaks + sel;
+  return TV_OK;
+}
+
+int tv_decode(const float* heat, const int64_t hs[4], const float* size, const int64_t ss[4], const float* offset,
+              const int64_t os[4], const float* depth, const int64_t ds[4], int32_t B, int32_t C, int32_t H, int32_t W,
+              int32_t K, int32_t mode, int32_t ratio, int32_t in_h, int32_t in_w, float thr, const float* aux,
+              const int64_t aux_st[5], float* records, int32_t* counts, void* ws, int64_t ws_bytes, void* stream) {
+  TV_GUARD({
+    int64_t need = 0;
+    int rc = tv_decode_workspace_size(B, C, H, W, K, &need);
+    if (rc) return rc;
+    if (!heat || !hs || !size || !ss || !records || !counts || !ws || ws_bytes < need) {
+      set_error("bad argument or workspace too small");
+      return TV_EINVAL;
+    }
+    if (mode == 0 && (!offset || !os)) { set_error("decode needs the offset head"); return TV_EINVAL; }
+    if (depth && !ds) { set_error("depth strides missing"); return TV_EINVAL; }
+    hipStream_t s = (hipStream_t)stream;
+    float* peaks = (float*)ws;
+    int64_t poff = ((int64_t)B * C * H * W * 4 + 255) / 256 * 256;
+    float* score = (float*)((char*)ws + poff);
+    int32_t* index = (int32_t*)((char*)ws + poff + (int64_t)B * K * 4);
+    rc = launch_peaks(heat, hs, B, C, H, W, 3, 1, peaks, s);
+    if (rc) return rc;
+    rc = launch_topk(peaks, B, (int64_t)C * H * W, K, score, index, s);
+    if (rc) return rc;
+    DecodeParams p{};
+    p.score = score;
+    p.index = index;
+    p.B = B; p.K = K; p.C = C; p.H = H; p.W = W;
+    p.size = size; p.size_st = ss;
+    p.offset = offset; p.offset_st = os;
+    p.depth = depth; p.depth_st = ds;
+    p.depth_mode = mode == 0 ? 0 : 1;
+    p.pos_mode = mode == 0 ? 0 : 1;
+    p.ratio = ratio; p.in_h = in_h; p.in_w = in_w;
+    p.out_h = ratio > 0 ? in_h / ratio : H;
+    p.out_w = ratio > 0 ? in_w / ratio : W;
+    p.score_thr = thr;
+    p.aux = aux;
+    if (aux) {
+      if (!aux_st) { set_error("aux strides missing"); return TV_EINVAL; }
+      for (int i = 0; i < 5; ++i) p.aux_st[i] = aux_st[i];
+    }
+    p.records = records;
+    p.counts = counts;
+    return launch_decode_records(p, s);
+  })
+}
+
+}  // extern "C"

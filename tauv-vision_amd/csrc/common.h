@@ -1,0 +1,99 @@
+// Shared definitions for the tauv-vision_amd HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+
+namespace tv {
+
+enum DType : int { F32 = 0, F16 = 1, BF16 = 2 };
+
+inline int dtype_size(int dt) { return dt == F32 ? 4 : 2; }
+
+// Thread-local error string behind tv_last_error().
+void set_error(const std::string& msg);
+
+#define TV_HIP(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      ::tv::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));              \
+      return 3; /* TV_EHIP */                                                           \
+    }                                                                                   \
+  } while (0)
+
+// ---- implicit-GEMM convolution ----------------------------------------------------
+// One K-segment of a fused GEMM: a kh x kw convolution (stride, pad) over an NHWC source
+// tensor. Several segments sum into one output (channel concat of Root, the 1x1 residual
+// branch of ResidualBlock fused into conv2's K).
+struct ConvSegment {
+  const void* src;  // element (b,y,x,c) at ((b*H + y)*W + x)*ldc + c
+  int H, W, C, ldc;
+  int kh, kw, stride, pad;
+  int ksteps;  // ceil(kh*kw*C / BK); BK = 128 bytes of elements
+  int kbase;   // first k-step of this segment in the packed weight rows
+};
+
+constexpr int kMaxSeg = 8;
+
+struct ConvParams {
+  ConvSegment seg[kMaxSeg];
+  int nseg;
+  int Ho, Wo, M;        // output grid of the GEMM (M = B*Ho*Wo pixels)
+  int N;                // GEMM columns actually stored (multiple of the 16-byte vector)
+  int Kpad;             // packed weight row length, elements
+  const void* weight;   // [Npad][Kpad] compute dtype
+  const float* bias;    // [Npad] fp32 (BN folded)
+  int act;              // 0 none, 1 relu, 2 leaky_relu(0.01)
+  void* out;            // mode 0: out pixel m at m*out_ldc + out_coff; mode 1: target grid
+  int out_ldc, out_coff;
+  int mtiles, ntiles;
+  // mode 1: non-overlapping ConvTranspose2d (k == s) phase scatter + add, with the
+  // pad_to_match shift (dla.py:195-209) folded into the target coordinates.
+  int up_s, up_cout;    // scale; output channels per phase (n = phase*up_cout + co)
+  int tH, tW, sy, sx;   // target grid and (row, col) shift
+  const void* add;      // tensor added at the target pixel (compute dtype)
+  int add_ldc;
+};
+
+// p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
+int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
+                hipStream_t s);
+
+// ---- small kernels -----------------------------------------------------------------
+int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad, int dtype,
+                     hipStream_t s);
+int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cpad, int dtype,
+                   hipStream_t s);
+// out[target] = add[target] for target pixels not covered by the shifted upsample.
+int launch_uncovered_copy(const void* add, int add_ldc, void* out, int out_ldc, int C, int B,
+                          int tH, int tW, int y0, int y1, int x0, int x1, int dtype,
+                          hipStream_t s);
+
+// ---- decode ------------------------------------------------------------------------
+int launch_peaks(const float* heat, const int64_t st[4], int B, int C, int H, int W, int k,
+                 int apply_sigmoid, float* peaks, hipStream_t s);
+int launch_topk(const float* peaks, int B, int64_t n, int K, float* score, int32_t* index,
+                hipStream_t s);
+struct DecodeParams {
+  const float* score;  // [B][K]
+  const int32_t* index;
+  int B, K, C, H, W;
+  const float* size;    const int64_t* size_st;    // element (b,y,x,ch) strides
+  const float* offset;  const int64_t* offset_st;  // may be null (keypoint object path)
+  const float* depth;   const int64_t* depth_st;   // may be null
+  int depth_mode;       // 0: 1/sigmoid(d) - 1 (decode), 1: 1/sigmoid(d) (decode_keypoints)
+  int ratio, in_h, in_w, out_h, out_w;
+  int pos_mode;         // 0: (R*i + offset)/in (decode), 1: i/out (decode_keypoints)
+  const float* aux;     // optional pair gather (keypoint affinity): element (b, label, j, y, x)
+  int64_t aux_st[5];
+  float score_thr;
+  float* records;       // [B][K][10]: label, score, y, x, h, w, depth, flat index, aux0, aux1
+  int32_t* counts;      // [B]
+};
+int launch_decode_records(const DecodeParams& p, hipStream_t s);
+// heatmap_detect()'s (index[B,K,2], label[B,K]) as int64 from flat top-K indices.
+int launch_index_split(const int32_t* flat, int B, int K, int H, int W, int64_t* index, int64_t* label,
+                       hipStream_t s);
+
+}  // namespace tv

@@ -1,0 +1,406 @@
+// Engine: BN folding + weight packing at create, liveness-planned HBM workspace per
+// (stream, batch), and the launch sequence of one forward. C ABI in capi.cpp.
+#include "engine.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <set>
+
+namespace tv {
+
+namespace {
+
+constexpr int kTile = 128;
+
+uint16_t f32_to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);  // NaN
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+void store_elem(void* base, size_t i, float v, int dtype) {
+  if (dtype == F32) {
+    reinterpret_cast<float*>(base)[i] = v;
+  } else if (dtype == F16) {
+    reinterpret_cast<_Float16*>(base)[i] = (_Float16)v;
+  } else {
+    reinterpret_cast<uint16_t*>(base)[i] = f32_to_bf16(v);
+  }
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+const float* Engine::weight(const std::string& name, int64_t numel) {
+  auto it = host_w.find(name);
+  if (it == host_w.end()) {
+    set_error("missing state_dict key: " + name);
+    return nullptr;
+  }
+  if (it->second.second != numel) {
+    set_error("state_dict key " + name + ": expected " + std::to_string(numel) + " elements, got " +
+              std::to_string(it->second.second));
+    return nullptr;
+  }
+  return it->second.first;
+}
+
+// Folded BN affine for a conv `p` (+ BatchNorm `bn`): scale, shift per output channel.
+int Engine::fold(const std::string& conv, const std::string& bn, int cout, std::vector<double>& scale,
+                 std::vector<double>& shift) {
+  scale.assign(cout, 1.0);
+  shift.assign(cout, 0.0);
+  const float* b = weight(conv + ".bias", cout);
+  if (!b) return TV_ENOTFOUND;
+  for (int i = 0; i < cout; ++i) shift[i] = b[i];
+  if (bn.empty()) return TV_OK;
+  const float* g = weight(bn + ".weight", cout);
+  const float* be = weight(bn + ".bias", cout);
+  const float* mu = weight(bn + ".running_mean", cout);
+  const float* var = weight(bn + ".running_var", cout);
+  if (!g || !be || !mu || !var) return TV_ENOTFOUND;
+  for (int i = 0; i < cout; ++i) {
+    double s = (double)g[i] / std::sqrt((double)var[i] + 1e-5);
+    scale[i] = s;
+    shift[i] = ((double)b[i] - (double)mu[i]) * s + (double)be[i];
+  }
+  return TV_OK;
+}
+
+int Engine::pack_op(size_t oi) {
+  const OpSpec& op = plan.ops[oi];
+  Packed& pk = packed[oi];
+  const int esz = dtype_size(dtype);
+  const int BK = 128 / esz;
+  if (op.kind == OP_PREP) return TV_OK;
+
+  std::vector<float> hw;    // [Npad][Kpad] fp32 staging
+  std::vector<float> bias;  // [Npad]
+  if (op.kind == OP_CONVT_ADD) {
+    const TensorSpec& src = plan.tensors[op.src];
+    const int c = op.N, s = op.up_s, cin = src.C;
+    const int N = s * s * c;
+    pk.Npad = (int)align_up(N, kTile);
+    pk.seg_ksteps = {(cin + BK - 1) / BK};
+    pk.Kpad = pk.seg_ksteps[0] * BK;
+    hw.assign((size_t)pk.Npad * pk.Kpad, 0.f);
+    bias.assign(pk.Npad, 0.f);
+    const float* w = weight(op.up_w + ".weight", (int64_t)cin * c * s * s);
+    const float* b = weight(op.up_w + ".bias", c);
+    if (!w || !b) return TV_ENOTFOUND;
+    for (int i = 0; i < s; ++i)
+      for (int j = 0; j < s; ++j)
+        for (int co = 0; co < c; ++co) {
+          const int n = (i * s + j) * c + co;
+          bias[n] = b[co];
+          for (int ci = 0; ci < cin; ++ci) hw[(size_t)n * pk.Kpad + ci] = w[(((size_t)ci * c + co) * s + i) * s + j];
+        }
+  } else {
+    const int N = op.N;
+    pk.Npad = (int)align_up(N, kTile);
+    int kbase = 0;
+    pk.seg_ksteps.clear();
+    for (const SegSpec& sg : op.segs) {
+      const int cs = plan.tensors[sg.src].C;
+      const int ks = (sg.kh * sg.kw * cs + BK - 1) / BK;
+      pk.seg_ksteps.push_back(ks);
+      kbase += ks;
+    }
+    pk.Kpad = kbase * BK;
+    hw.assign((size_t)pk.Npad * pk.Kpad, 0.f);
+    bias.assign(pk.Npad, 0.f);
+    if (!op.stack_w.empty()) {
+      // stacked heads (3x3, single segment) or block-diagonal 1x1 heads
+      const SegSpec& sg = op.segs[0];
+      const int cs = plan.tensors[sg.src].C;
+      const bool diag = !op.diag_in_off.empty();
+      int row = 0;
+      for (size_t h = 0; h < op.stack_w.size(); ++h) {
+        const int n = op.stack_n[h];
+        const int cin = diag ? plan.tensors[sg.src].C / (int)op.stack_w.size() : sg.cin;
+        const int k = sg.kh;
+        const float* w = weight(op.stack_w[h] + ".weight", (int64_t)n * cin * k * k);
+        const float* b = weight(op.stack_w[h] + ".bias", n);
+        if (!w || !b) return TV_ENOTFOUND;
+        const int r0 = diag ? op.diag_out_off[h] : row;
+        const int c0 = diag ? op.diag_in_off[h] : 0;
+        for (int co = 0; co < n; ++co) {
+          bias[r0 + co] = b[co];
+          for (int ci = 0; ci < cin; ++ci)
+            for (int t = 0; t < k * k; ++t)
+              hw[(size_t)(r0 + co) * pk.Kpad + t * cs + c0 + ci] = w[((size_t)co * cin + ci) * k * k + t];
+        }
+        row += n;
+      }
+    } else {
+      // BN-folded segments; bias = sum over the distinct convs feeding this GEMM
+      std::set<std::string> seen;
+      int kb = 0;
+      for (size_t si = 0; si < op.segs.size(); ++si) {
+        const SegSpec& sg = op.segs[si];
+        const int cs = plan.tensors[sg.src].C;
+        // total input channels of the PyTorch weight = max over segments sharing it
+        int wcin = 0;
+        for (const SegSpec& o : op.segs)
+          if (o.wname == sg.wname) wcin = std::max(wcin, o.ci0 + o.cin);
+        const int kk = sg.kh * sg.kw;
+        const float* w = weight(sg.wname + ".weight", (int64_t)N * wcin * kk);
+        if (!w) return TV_ENOTFOUND;
+        std::vector<double> scale, shift;
+        int rc = fold(sg.wname, sg.bn, N, scale, shift);
+        if (rc) return rc;
+        if (seen.insert(sg.wname).second)
+          for (int co = 0; co < N; ++co) bias[co] += (float)shift[co];
+        for (int co = 0; co < N; ++co)
+          for (int ci = 0; ci < sg.cin; ++ci)
+            for (int t = 0; t < kk; ++t)
+              hw[(size_t)co * pk.Kpad + (size_t)kb * BK + t * cs + ci] =
+                  (float)((double)w[((size_t)co * wcin + sg.ci0 + ci) * kk + t] * scale[co]);
+        kb += pk.seg_ksteps[si];
+      }
+    }
+  }
+  // device copies
+  std::vector<uint8_t> hbuf((size_t)pk.Npad * pk.Kpad * esz);
+  for (size_t i = 0; i < hw.size(); ++i) store_elem(hbuf.data(), i, hw[i], dtype);
+  TV_HIP(hipMalloc(&pk.w, hbuf.size()));
+  TV_HIP(hipMemcpy(pk.w, hbuf.data(), hbuf.size(), hipMemcpyHostToDevice));
+  TV_HIP(hipMalloc((void**)&pk.bias, bias.size() * sizeof(float)));
+  TV_HIP(hipMemcpy(pk.bias, bias.data(), bias.size() * sizeof(float), hipMemcpyHostToDevice));
+  weight_bytes += hbuf.size() + bias.size() * 4;
+  return TV_OK;
+}
+
+int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev) {
+  desc = d;
+  device = dev;
+  dtype = d.compute_dtype;
+  int rc = build_plan(d, &plan);
+  if (rc) return rc;
+  for (int i = 0; i < n; ++i) {
+    if (!w[i].name || (!w[i].data && w[i].numel)) {
+      set_error("null weight view");
+      return TV_EINVAL;
+    }
+    host_w[w[i].name] = {w[i].data, w[i].numel};
+  }
+  TV_HIP(hipSetDevice(device));
+  packed.resize(plan.ops.size());
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    rc = pack_op(i);
+    if (rc) return rc;
+  }
+  host_w.clear();  // views are only valid during create
+  return TV_OK;
+}
+
+Engine::~Engine() {
+  for (auto& p : packed) {
+    if (p.w) (void)hipFree(p.w);
+    if (p.bias) (void)hipFree(p.bias);
+  }
+  for (auto& kv : workspaces) {
+    if (kv.second->arena) (void)hipFree(kv.second->arena);
+    if (kv.second->dparams) (void)hipFree(kv.second->dparams);
+    delete kv.second;
+  }
+}
+
+// Liveness-planned arena: a tensor lives from its producing op to its last reader;
+// first-fit placement of each new tensor into the gaps left by dead ones.
+int Engine::make_workspace(int B, Workspace* ws) {
+  const int esz = dtype_size(dtype);
+  const size_t nt = plan.tensors.size();
+  std::vector<int> def(nt, -1), last(nt, -1);
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    if (op.out >= 0) def[op.out] = (int)i, last[op.out] = std::max(last[op.out], (int)i);
+    for (const SegSpec& s : op.segs) last[s.src] = std::max(last[s.src], (int)i);
+    if (op.kind == OP_CONVT_ADD) {
+      last[op.src] = std::max(last[op.src], (int)i);
+      last[op.add] = std::max(last[op.add], (int)i);
+    }
+  }
+  ws->off.assign(nt, 0);
+  struct Live { size_t off, size; int last; };
+  std::vector<Live> live;
+  size_t peak = 0;
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    live.erase(std::remove_if(live.begin(), live.end(), [&](const Live& l) { return l.last < (int)i; }), live.end());
+    if (op.out < 0) continue;
+    const TensorSpec& t = plan.tensors[op.out];
+    size_t sz = align_up((size_t)B * t.H * t.W * t.C * esz, 256);
+    std::sort(live.begin(), live.end(), [](const Live& a, const Live& b) { return a.off < b.off; });
+    size_t pos = 0;
+    for (const Live& l : live) {
+      if (pos + sz <= l.off) break;
+      pos = std::max(pos, l.off + l.size);
+    }
+    ws->off[op.out] = pos;
+    live.push_back({pos, sz, last[op.out]});
+    peak = std::max(peak, pos + sz);
+  }
+  ws->bytes = peak;
+  ws->B = B;
+  TV_HIP(hipSetDevice(device));
+  TV_HIP(hipMalloc(&ws->arena, std::max<size_t>(peak, 256)));
+  // launch parameters for every op
+  ws->params.assign(plan.ops.size(), ConvParams{});
+  char* base = (char*)ws->arena;
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    if (op.kind == OP_PREP) continue;
+    ConvParams& p = ws->params[i];
+    const Packed& pk = packed[i];
+    std::memset(&p, 0, sizeof(p));
+    p.weight = pk.w;
+    p.bias = pk.bias;
+    p.Kpad = pk.Kpad;
+    p.act = op.act;
+    int kbase = 0;
+    if (op.kind == OP_CONV) {
+      p.nseg = (int)op.segs.size();
+      for (size_t s = 0; s < op.segs.size(); ++s) {
+        const SegSpec& sg = op.segs[s];
+        const TensorSpec& t = plan.tensors[sg.src];
+        p.seg[s] = ConvSegment{base + ws->off[sg.src], t.H, t.W, t.C, t.C, sg.kh, sg.kw, sg.stride, sg.pad,
+                               pk.seg_ksteps[s], kbase};
+        kbase += pk.seg_ksteps[s];
+      }
+      const int Ho = op.out >= 0 ? plan.tensors[op.out].H : plan.out_h;
+      const int Wo = op.out >= 0 ? plan.tensors[op.out].W : plan.out_w;
+      p.Ho = Ho;
+      p.Wo = Wo;
+      p.M = B * Ho * Wo;
+      p.N = op.N;
+      p.out = op.out >= 0 ? (void*)(base + ws->off[op.out]) : nullptr;  // patched per call
+      p.out_ldc = op.out >= 0 ? plan.tensors[op.out].C : plan.out_cpad;
+      p.out_coff = 0;
+      p.mtiles = (p.M + kTile - 1) / kTile;
+      p.ntiles = pk.Npad / kTile;
+    } else {
+      const TensorSpec& src = plan.tensors[op.src];
+      const TensorSpec& tgt = plan.tensors[op.out];
+      p.nseg = 1;
+      p.seg[0] = ConvSegment{base + ws->off[op.src], src.H, src.W, src.C, src.C, 1, 1, 1, 0, pk.seg_ksteps[0], 0};
+      p.Ho = src.H;
+      p.Wo = src.W;
+      p.M = B * src.H * src.W;
+      p.N = op.up_s * op.up_s * op.N;
+      p.out = base + ws->off[op.out];
+      p.out_ldc = tgt.C;
+      p.mtiles = (p.M + kTile - 1) / kTile;
+      p.ntiles = (p.N + kTile - 1) / kTile;
+      p.up_s = op.up_s;
+      p.up_cout = op.N;
+      p.tH = tgt.H;
+      p.tW = tgt.W;
+      p.sy = op.sy;
+      p.sx = op.sx;
+      p.add = base + ws->off[op.add];
+      p.add_ldc = plan.tensors[op.add].C;
+    }
+  }
+  TV_HIP(hipMalloc((void**)&ws->dparams, ws->params.size() * sizeof(ConvParams)));
+  TV_HIP(hipMemcpy(ws->dparams, ws->params.data(), ws->params.size() * sizeof(ConvParams), hipMemcpyHostToDevice));
+  return TV_OK;
+}
+
+int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
+  std::lock_guard<std::mutex> g(mu);
+  auto key = std::make_pair((void*)stream, B);
+  auto it = workspaces.find(key);
+  if (it != workspaces.end()) {
+    *out = it->second;
+    return TV_OK;
+  }
+  Workspace* ws = new Workspace();
+  int rc = make_workspace(B, ws);
+  if (rc) {
+    if (ws->arena) (void)hipFree(ws->arena);
+    if (ws->dparams) (void)hipFree(ws->dparams);
+    delete ws;
+    return rc;
+  }
+  workspaces[key] = ws;
+  *out = ws;
+  return TV_OK;
+}
+
+int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, float* out, hipStream_t s) {
+  const OpSpec& op = plan.ops[i];
+  char* base = (char*)ws->arena;
+  if (op.kind == OP_PREP) {
+    void* dst = base + ws->off[op.out];
+    return input_u8 ? launch_prep_u8((const uint8_t*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s)
+                    : launch_prep_nchw((const float*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s);
+  }
+  ConvParams p = ws->params[i];
+  if (op.out < 0) p.out = out;
+  const bool out_f32 = op.out < 0;
+  int rc = launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, op.kind == OP_CONVT_ADD ? 1 : 0, s);
+  if (rc) return rc;
+  if (op.kind == OP_CONVT_ADD) {
+    const TensorSpec& tgt = plan.tensors[op.out];
+    if (op.cov_y0 > 0 || op.cov_x0 > 0 || op.cov_y1 < tgt.H || op.cov_x1 < tgt.W)
+      return launch_uncovered_copy(p.add, p.add_ldc, p.out, p.out_ldc, tgt.C, ws->B, tgt.H, tgt.W, op.cov_y0,
+                                   op.cov_y1, op.cov_x0, op.cov_x1, dtype, s);
+  }
+  return TV_OK;
+}
+
+int Engine::forward(const void* input, int input_u8, int B, float* out, hipStream_t s) {
+  if (B < 1) {
+    set_error("batch must be >= 1");
+    return TV_EINVAL;
+  }
+  if (!input || !out) {
+    set_error("null input/output pointer");
+    return TV_EINVAL;
+  }
+  TV_HIP(hipSetDevice(device));
+  Workspace* ws = nullptr;
+  int rc = get_workspace(B, s, &ws);
+  if (rc) return rc;
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    rc = run_op(i, ws, input, input_u8, out, s);
+    if (rc) return rc;
+  }
+  return TV_OK;
+}
+
+int Engine::profile(const float* img, int B, float* out, hipStream_t s, float* ms, double* flops, int cap,
+                    int* n_ops) {
+  TV_HIP(hipSetDevice(device));
+  Workspace* ws = nullptr;
+  int rc = get_workspace(B, s, &ws);
+  if (rc) return rc;
+  const size_t n = plan.ops.size();
+  std::vector<hipEvent_t> ev(n + 1);
+  for (auto& e : ev) TV_HIP(hipEventCreate(&e));
+  TV_HIP(hipEventRecord(ev[0], s));
+  for (size_t i = 0; i < n; ++i) {
+    rc = run_op(i, ws, img, 0, out, s);
+    if (rc) break;
+    TV_HIP(hipEventRecord(ev[i + 1], s));
+  }
+  if (!rc) {
+    TV_HIP(hipEventSynchronize(ev[n]));
+    for (size_t i = 0; i < n && (int)i < cap; ++i) {
+      float t = 0;
+      TV_HIP(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      ms[i] = t;
+      flops[i] = plan.ops[i].flops * B;
+    }
+    *n_ops = (int)n;
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return rc;
+}
+
+}  // namespace tv

@@ -1,0 +1,56 @@
+#pragma once
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+#include "planner.h"
+
+namespace tv {
+
+struct Packed {
+  void* w = nullptr;       // [Npad][Kpad] compute dtype
+  float* bias = nullptr;   // [Npad]
+  int Npad = 0, Kpad = 0;
+  std::vector<int> seg_ksteps;
+};
+
+struct Workspace {
+  int B = 0;
+  void* arena = nullptr;
+  size_t bytes = 0;
+  std::vector<size_t> off;          // per tensor
+  std::vector<ConvParams> params;   // per op (host copy)
+  ConvParams* dparams = nullptr;    // per op (device copy)
+};
+
+struct Engine {
+  tv_model_desc desc{};
+  Plan plan;
+  int device = 0;
+  int dtype = F32;
+  std::vector<Packed> packed;  // per op
+  size_t weight_bytes = 0;
+  std::mutex mu;
+  std::map<std::pair<void*, int>, Workspace*> workspaces;
+  std::unordered_map<std::string, std::pair<const float*, int64_t>> host_w;  // during create only
+
+  ~Engine();
+  int create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev);
+  int get_workspace(int B, hipStream_t s, Workspace** out);
+  int forward(const void* input, int input_u8, int B, float* out, hipStream_t s);
+  int profile(const float* img, int B, float* out, hipStream_t s, float* ms, double* flops, int cap, int* n_ops);
+
+ private:
+  const float* weight(const std::string& name, int64_t numel);
+  int fold(const std::string& conv, const std::string& bn, int cout, std::vector<double>& scale,
+           std::vector<double>& shift);
+  int pack_op(size_t i);
+  int make_workspace(int B, Workspace* ws);
+  int run_op(size_t i, Workspace* ws, const void* input, int input_u8, float* out, hipStream_t s);
+};
+
+}  // namespace tv

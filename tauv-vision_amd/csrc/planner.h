@@ -1,0 +1,66 @@
+// Network planner for the reference "R18" CenterNet (Centernet + DLABackbone):
+// enumerates the reference state_dict layout and lowers the forward pass to a list of
+// fused GEMM launches over NHWC tensors.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/tauv_vision_amd.h"
+
+namespace tv {
+
+struct ParamInfo {
+  std::string name;
+  std::vector<int64_t> shape;
+};
+
+// One K-segment of a fused conv: input channels [ci0, ci0 + cin) of a PyTorch conv weight,
+// applied to tensor `src` (whose stored channel count may be padded beyond cin).
+struct SegSpec {
+  int src;               // tensor id
+  std::string wname;     // "<prefix>.weight" of the Conv2d
+  std::string bn;        // BatchNorm2d prefix folded into this conv ("" = none)
+  int ci0, cin;          // slice of the weight's input channels
+  int kh, kw, stride, pad;
+};
+
+enum OpKind { OP_PREP = 0, OP_CONV = 1, OP_CONVT_ADD = 2 };
+
+struct OpSpec {
+  int kind;
+  std::string label;          // human-readable (reference module path)
+  std::vector<SegSpec> segs;  // OP_CONV
+  int out;                    // tensor id (-1 = the caller's fp32 output buffer)
+  int N;                      // output channels (GEMM columns before phase expansion)
+  int act;                    // 0 none, 1 relu, 2 leaky
+  // head fusion: weights of several convs stacked along N (names in order, N each)
+  std::vector<std::string> stack_w;
+  std::vector<int> stack_n;
+  // final block-diagonal 1x1 heads: weight j feeds output channels [out_off[j], +n) from
+  // input channels [in_off[j], +cin)
+  std::vector<int> diag_in_off, diag_out_off;
+  // OP_CONVT_ADD
+  int src = -1, add = -1, up_s = 0, sy = 0, sx = 0;
+  std::string up_w;           // ConvTranspose2d prefix
+  int cov_y0 = 0, cov_y1 = 0, cov_x0 = 0, cov_x1 = 0;  // covered target rectangle
+  double flops = 0;           // algorithmic FLOPs per frame (2*MAC)
+};
+
+struct TensorSpec {
+  int H, W, C;  // per frame, stored channels (ldc == C)
+};
+
+struct Plan {
+  std::vector<ParamInfo> params;     // reference state_dict order
+  std::vector<TensorSpec> tensors;
+  std::vector<OpSpec> ops;
+  int out_h = 0, out_w = 0, out_c = 0, out_cpad = 0;
+  int in_cpad = 0;
+  double flops_per_frame = 0;
+};
+
+// Returns 0 or a TV_E* code (with tv_last_error set).
+int build_plan(const tv_model_desc& d, Plan* plan);
+
+}  // namespace tv

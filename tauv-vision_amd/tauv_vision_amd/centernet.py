@@ -1,0 +1,185 @@
+"""Drop-in `Centernet` / `Prediction` / `get_head_channels` (reference
+src/tauv_vision/centernet/model/centernet.py:13-142) backed by the native MI355X engine.
+
+The module keeps the reference state_dict layout exactly (keys, shapes, order), so
+`load_state_dict(torch.load(path))` of a reference checkpoint works unchanged; the
+forward pass is one native call (all convolutions as fused MFMA implicit GEMMs, see
+csrc/planner.cpp) and returns the reference's `Prediction`, whose tensors are channel
+slices of one fp32 NHWC head tensor (same shapes and values, different strides).
+"""
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .config import ObjectConfigSet
+from .dla import DLABackbone, populate
+from .engine import NativeEngine
+from .weights import model_desc, param_layout
+
+
+@dataclass
+class Prediction:
+    heatmap: torch.Tensor                      # [B, n_labels, out_h, out_w]
+    keypoint_heatmap: Optional[torch.Tensor]   # [B, n_keypoints, out_h, out_w]
+    keypoint_affinity: Optional[torch.Tensor]  # [B, n_keypoints, 2, out_h, out_w]
+    size: torch.Tensor                         # [B, out_h, out_w, 2]
+    offset: torch.Tensor                       # [B, out_h, out_w, 2]
+    roll_bin: Optional[torch.Tensor]           # [B, out_h, out_w, 4]
+    roll_offset: Optional[torch.Tensor]
+    pitch_bin: Optional[torch.Tensor]
+    pitch_offset: Optional[torch.Tensor]
+    yaw_bin: Optional[torch.Tensor]
+    yaw_offset: Optional[torch.Tensor]
+    depth: Optional[torch.Tensor]              # [B, out_h, out_w, 1]
+
+
+def get_head_channels(object_config: ObjectConfigSet) -> List[int]:
+    """centernet.py:114-142: heatmap, [keypoint heatmap, keypoint affinity], size, offset,
+    [yaw bin/offset], [pitch bin/offset], [roll bin/offset], [depth]."""
+    out = [object_config.n_labels]
+    if object_config.train_keypoints:
+        out += [object_config.n_keypoints, 2 * object_config.n_keypoints]
+    out += [2, 2]
+    for flag in (object_config.train_yaw, object_config.train_pitch, object_config.train_roll):
+        if flag:
+            out += [4, 4]
+    if object_config.train_depth:
+        out.append(1)
+    return out
+
+
+def prediction_fields(object_config: ObjectConfigSet):
+    """Field -> (first channel, channel count), following the reference's pop order
+    (centernet.py:77-90): after size/offset it assigns roll, pitch, yaw — although
+    get_head_channels created the angle heads yaw, pitch, roll — then depth."""
+    widths = get_head_channels(object_config)
+    starts = [sum(widths[:i]) for i in range(len(widths))]
+    order = ["heatmap"]
+    if object_config.train_keypoints:
+        order += ["keypoint_heatmap", "keypoint_affinity"]
+    order += ["size", "offset"]
+    for axis, flag in (("roll", object_config.train_roll), ("pitch", object_config.train_pitch),
+                       ("yaw", object_config.train_yaw)):
+        if flag:
+            order += [f"{axis}_bin", f"{axis}_offset"]
+    if object_config.train_depth:
+        order.append("depth")
+    return {name: (starts[i], widths[i]) for i, name in enumerate(order)}
+
+
+def prediction_from_nhwc(out: torch.Tensor, object_config: ObjectConfigSet) -> Prediction:
+    fields = {f: None for f in Prediction.__dataclass_fields__}
+    for name, (s, n) in prediction_fields(object_config).items():
+        t = out[..., s:s + n]
+        if name in ("heatmap", "keypoint_heatmap"):
+            t = t.permute(0, 3, 1, 2)
+        elif name == "keypoint_affinity":
+            B, H, W, _ = t.shape
+            t = t.unflatten(3, (n // 2, 2)).permute(0, 3, 4, 1, 2)
+        fields[name] = t
+    return Prediction(**fields)
+
+
+class Centernet(nn.Module):
+    """centernet.py:32-92. `precision`: "fp32" (exact-f32 MFMA, parity mode), "fp16" or
+    "bf16" (fp32 accumulation; throughput mode)."""
+
+    def __init__(self, backbone: DLABackbone, object_config: ObjectConfigSet, precision: str = "fp32"):
+        super().__init__()
+        self.backbone = backbone
+        self.object_config = object_config
+        self.head_channels = get_head_channels(object_config)
+        if precision not in _lib.DTYPES:
+            raise ValueError(f"precision must be one of {sorted(_lib.DTYPES)}")
+        self.precision = precision
+        desc = model_desc(backbone.heights, backbone.channels, backbone.downsamples, self.head_channels)
+        layout = [(k, s) for k, s in param_layout(desc) if k.startswith("heads.")]
+        self.heads = nn.Module()
+        populate(self.heads, [(k[len("heads."):], s) for k, s in layout], seed_layout=layout, prefix="heads.")
+        self._version = [0]
+        self._engines = {}
+        self.register_load_state_dict_post_hook(lambda module, keys: module.invalidate())
+
+    # -- engine cache ---------------------------------------------------------------
+    def invalidate(self):
+        self._version[0] += 1
+        self._engines = {}
+
+    def _apply(self, fn, *args, **kwargs):
+        r = super()._apply(fn, *args, **kwargs)
+        self.invalidate()
+        return r
+
+    def set_precision(self, precision: str):
+        if precision not in _lib.DTYPES:
+            raise ValueError(f"precision must be one of {sorted(_lib.DTYPES)}")
+        self.precision = precision
+        self.invalidate()
+        return self
+
+    def _device_for(self, t: torch.Tensor) -> torch.device:
+        if not torch.cuda.is_available():
+            raise RuntimeError("tauv_vision_amd needs a gfx950 (MI355X) GPU; no HIP device is visible")
+        if t.is_cuda:
+            return t.device
+        p = next(self.parameters())
+        return p.device if p.is_cuda else torch.device("cuda", torch.cuda.current_device())
+
+    def engine(self, device: torch.device, in_h: int, in_w: int) -> NativeEngine:
+        key = (device.index if device.index is not None else torch.cuda.current_device(), in_h, in_w,
+               self.precision, self._version[0], self.backbone._version[0])
+        eng = self._engines.get(key)
+        if eng is None:
+            desc = model_desc(self.backbone.heights, self.backbone.channels, self.backbone.downsamples,
+                              self.head_channels, in_h, in_w, self.precision)
+            eng = NativeEngine(desc, self.state_dict(), key[0])
+            self._engines = {key: eng}
+        return eng
+
+    # -- reference API --------------------------------------------------------------
+    def forward(self, img: torch.Tensor) -> Prediction:
+        if img.dim() != 4 or img.shape[1] != 3:
+            raise ValueError(f"expected img [batch, 3, in_h, in_w], got {tuple(img.shape)}")
+        dev = self._device_for(img)
+        img = img.to(dev, torch.float32).contiguous()
+        eng = self.engine(dev, img.shape[2], img.shape[3])
+        return prediction_from_nhwc(eng.forward(img), self.object_config)
+
+    def forward_frames(self, frames: torch.Tensor) -> Prediction:
+        """Raw uint8 RGB frames [B, H, W, 3] (or [H, W, 3]) with the node's ToTensor +
+        ImageNet Normalize (centernet_node.py:90-92) fused into the first kernel."""
+        if frames.dim() == 3:
+            frames = frames.unsqueeze(0)
+        if frames.dtype != torch.uint8 or frames.shape[-1] != 3:
+            raise ValueError("frames must be uint8 [B, H, W, 3]")
+        dev = self._device_for(frames)
+        frames = frames.to(dev).contiguous()
+        eng = self.engine(dev, frames.shape[1], frames.shape[2])
+        return prediction_from_nhwc(eng.forward_u8(frames), self.object_config)
+
+    def detect(self, frames: torch.Tensor, model_config, n_detections: int = 100, score_threshold: float = 0.3):
+        """detect(frames) == decode(forward(preprocess(frames)), ...)."""
+        from .decode import decode
+        return decode(self.forward_frames(frames), model_config, n_detections, score_threshold)
+
+
+def initialize_weights(module: nn.Module, excluded_modules=()):
+    """centernet.py:103-111 analogue: re-draw every conv/conv-transpose weight xavier-uniform
+    and zero its bias (parameter tree leaves with a 4-D weight)."""
+    excluded = set()
+    for m in excluded_modules:
+        excluded.update(id(x) for x in m.modules())
+    for sub in module.modules():
+        w = sub._parameters.get("weight") if hasattr(sub, "_parameters") else None
+        if w is not None and w.dim() == 4 and id(sub) not in excluded:
+            with torch.no_grad():
+                nn.init.xavier_uniform_(w)
+                b = sub._parameters.get("bias")
+                if b is not None:
+                    b.zero_()
+    for m in module.modules():
+        if isinstance(m, Centernet):
+            m.invalidate()

@@ -1,0 +1,83 @@
+"""Owning wrapper of one native engine (tv_engine_*): built from reference-layout weights
+for one (device, input size, precision); forward launches on the caller's torch stream."""
+import ctypes
+
+import torch
+
+from . import _lib
+from .weights import geometry
+
+
+class NativeEngine:
+    def __init__(self, desc, state_dict, device_index):
+        self.desc = desc
+        self.device = torch.device("cuda", device_index)
+        self.geom = geometry(desc)
+        host = {k: v.detach().to("cpu", torch.float32).contiguous() for k, v in state_dict.items()
+                if v.dtype.is_floating_point}
+        views = (_lib.WeightView * len(host))()
+        keep = []
+        for i, (k, v) in enumerate(host.items()):
+            name = k.encode()
+            keep.append(name)
+            views[i].name = name
+            views[i].data = v.data_ptr()
+            views[i].numel = v.numel()
+        handle = ctypes.c_void_p()
+        L = _lib.lib()
+        with torch.cuda.device(self.device):
+            _lib.check(L.tv_engine_create(ctypes.byref(desc), views, len(host), device_index, ctypes.byref(handle)),
+                       "engine create")
+        self._h = handle
+        del keep, host
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.tv_engine_destroy(h)
+            self._h = None
+
+    @property
+    def out_shape_per_frame(self):
+        g = self.geom
+        return g["out_h"], g["out_w"], g["out_cpad"]
+
+    def alloc_out(self, batch):
+        oh, ow, oc = self.out_shape_per_frame
+        return torch.empty((batch, oh, ow, oc), dtype=torch.float32, device=self.device)
+
+    def prepare(self, batch):
+        _lib.check(_lib.lib().tv_engine_prepare(self._h, int(batch), _lib.stream_of(self.device)), "prepare")
+
+    def forward(self, img, out=None):
+        """img: fp32 NCHW on this device; returns the fp32 NHWC head tensor."""
+        B = img.shape[0]
+        if out is None:
+            out = self.alloc_out(B)
+        _lib.check(_lib.lib().tv_engine_forward(self._h, ctypes.c_void_p(img.data_ptr()), B,
+                                                ctypes.c_void_p(out.data_ptr()), _lib.stream_of(self.device)),
+                   "forward")
+        return out
+
+    def forward_u8(self, frames, out=None):
+        """frames: uint8 NHWC RGB on this device (ToTensor + ImageNet Normalize fused)."""
+        B = frames.shape[0]
+        if out is None:
+            out = self.alloc_out(B)
+        _lib.check(_lib.lib().tv_engine_forward_u8(self._h, ctypes.c_void_p(frames.data_ptr()), B,
+                                                   ctypes.c_void_p(out.data_ptr()), _lib.stream_of(self.device)),
+                   "forward_u8")
+        return out
+
+    def profile(self, img, out=None, cap=4096):
+        """Per-launch (label, ms, flops) of one forward, timed with HIP events."""
+        B = img.shape[0]
+        if out is None:
+            out = self.alloc_out(B)
+        ms = (ctypes.c_float * cap)()
+        fl = (ctypes.c_double * cap)()
+        n = ctypes.c_int32()
+        L = _lib.lib()
+        _lib.check(L.tv_engine_profile(self._h, ctypes.c_void_p(img.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
+                                       _lib.stream_of(self.device), ms, fl, cap, ctypes.byref(n)), "profile")
+        return [(L.tv_engine_op_label(self._h, i).decode(), ms[i], fl[i]) for i in range(min(n.value, cap))]

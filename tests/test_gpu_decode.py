@@ -1,0 +1,137 @@
+"""GPU parity of the decode kernels (peak NMS, exact top-K, records) against the
+reference's golden vectors and the CPU oracle. Bit-exact indices; fp32 values."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import golden
+from recipe import decode_case_inputs, gaussian_blob
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["decode_b3_c4_120x160", "decode_b2_c4_90x160", "decode_b1_c80_64x64"]
+
+
+def _inputs(name):
+    g = golden(name)
+    seed, B, C, H, W = [int(v) for v in g["seed"]]
+    return g, decode_case_inputs(B, C, H, W, seed)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_nms_and_topk_match_golden(name):
+    from tauv_vision_amd import heatmap_nms, heatmap_detect
+    g, (logits, size, offset, depth) = _inputs(name)
+    sig = torch.sigmoid(logits).cuda()
+    nms = heatmap_nms(sig, 3)
+    # peak set bit-exact; values are the input values (no arithmetic)
+    np.testing.assert_array_equal(nms.cpu().numpy(), g["nms"])
+    idx, lab, score = heatmap_detect(nms, 100)
+    np.testing.assert_array_equal(idx.cpu().numpy(), g["index"])
+    np.testing.assert_array_equal(lab.cpu().numpy(), g["label"])
+    np.testing.assert_array_equal(score.cpu().numpy(), g["score"])
+    assert idx.dtype == torch.int64 and lab.dtype == torch.int64 and score.dtype == torch.float32
+
+
+class _P:
+    pass
+
+
+def _check(got, ref, has_depth, tol=1e-5):
+    B = ref.shape[0]
+    for b in range(B):
+        n_ref = int(np.nansum(ref[b, :, 7]))
+        assert len(got[b]) == n_ref, (b, len(got[b]), n_ref)
+        for i, d in enumerate(got[b]):
+            assert int(d.label) == int(ref[b, i, 0])
+            assert isinstance(d.label, torch.Tensor) and d.label.dim() == 0
+            np.testing.assert_allclose(float(d.score), ref[b, i, 1], rtol=0, atol=1e-6)
+            np.testing.assert_allclose([d.y, d.x, d.h, d.w], ref[b, i, 2:6], rtol=tol, atol=tol)
+            if has_depth:
+                np.testing.assert_allclose(d.depth, ref[b, i, 6], rtol=1e-5, atol=1e-5)
+            else:
+                assert d.depth is None
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_decode_matches_golden(name):
+    import tauv_vision_amd as tv
+    g, (logits, size, offset, depth) = _inputs(name)
+    in_h, in_w, ds = [int(v) for v in g["meta"]]
+    mc = tv.ModelConfig([], [], in_h, in_w, ds, 1.0)
+    p = _P()
+    p.heatmap, p.size, p.offset, p.depth = logits.cuda(), size.cuda(), offset.cuda(), depth.cuda()
+    for thr in (0.05, 0.3, 0.9):
+        _check(tv.decode(p, mc, 100, thr), g[f"decode_thr{thr}"], True)
+    p.depth = None
+    _check(tv.decode(p, mc, 100, 0.3), g["decode_nodepth_thr0.3"], False)
+
+
+def test_decode_strided_nhwc_views():
+    """The engine hands decode NHWC channel-slice views; results must not depend on strides."""
+    import tauv_vision_amd as tv
+    g, (logits, size, offset, depth) = _inputs("decode_b3_c4_120x160")
+    nhwc = torch.cat([logits.permute(0, 2, 3, 1), size, offset, depth], dim=3).contiguous().cuda()
+    p = _P()
+    p.heatmap = nhwc[..., 0:4].permute(0, 3, 1, 2)
+    p.size, p.offset, p.depth = nhwc[..., 4:6], nhwc[..., 6:8], nhwc[..., 8:9]
+    mc = tv.ModelConfig([], [], 480, 640, 2, 1.0)
+    _check(tv.decode(p, mc, 100, 0.3), g["decode_thr0.3"], True)
+
+
+def test_kat_two_blobs():
+    """decode.py:327-339 known-answer test (restated Gaussian)."""
+    from tauv_vision_amd import heatmap_nms, heatmap_detect
+    h = torch.cat((gaussian_blob(512, 512, 100, 100, 50)[None, None],
+                   gaussian_blob(512, 512, 200, 200, 50)[None, None]), dim=1).cuda()
+    idx, lab, score = heatmap_detect(heatmap_nms(h, 3), 100)
+    g = golden("kat_two_blobs")
+    np.testing.assert_array_equal(idx[:, :2].cpu().numpy(), g["index"])
+    np.testing.assert_array_equal(lab[:, :2].cpu().numpy(), g["label"])
+    np.testing.assert_array_equal(score[:, :2].cpu().numpy(), g["score"])
+    assert idx[0, 0].tolist() == [100, 100]
+
+
+def test_topk_edge_cases():
+    from tauv_vision_amd import heatmap_detect, heatmap_nms
+    # all zeros: ties everywhere -> the K smallest flat indices (deterministic tie rule)
+    z = torch.zeros(2, 3, 7, 9, device="cuda")
+    idx, lab, score = heatmap_detect(z, 20)
+    flat = (lab * 63 + idx[..., 0] * 9 + idx[..., 1]).cpu()
+    assert torch.equal(flat, torch.arange(20).repeat(2, 1))
+    assert float(score.abs().sum()) == 0.0
+    # K == n and K == 1 against a full sort of distinct values
+    x = torch.randperm(2 * 3 * 7 * 9).float().reshape(2, 3, 7, 9).cuda()
+    for K in (1, 189):
+        idx, lab, score = heatmap_detect(x, K)
+        ref = torch.sort(x.reshape(2, -1), dim=1, descending=True)
+        np.testing.assert_array_equal(score.cpu().numpy(), ref.values[:, :K].cpu().numpy())
+        flat = lab * 63 + idx[..., 0] * 9 + idx[..., 1]
+        np.testing.assert_array_equal(flat.cpu().numpy(), ref.indices[:, :K].cpu().numpy())
+    with pytest.raises(RuntimeError):
+        heatmap_detect(x, 190)
+    with pytest.raises(AssertionError):
+        heatmap_nms(x, 2)
+    # heavy ties: one value repeated far beyond the LDS bucket (> 4096 equal keys)
+    big = torch.full((1, 4, 64, 64), 0.5, device="cuda")
+    big[0, 1, 5, 7] = 0.75
+    idx, lab, score = heatmap_detect(big, 300)
+    assert (lab[0, 0].item(), idx[0, 0].tolist()) == (1, [5, 7])
+    flat = (lab * 4096 + idx[..., 0] * 64 + idx[..., 1])[0, 1:].cpu()
+    assert torch.equal(flat, torch.arange(299))
+    # negative values and k=1 / k=5 windows against the oracle
+    y = torch.randn(2, 3, 17, 23)
+    for k in (1, 3, 5):
+        np.testing.assert_array_equal(heatmap_nms(y.cuda(), k).cpu().numpy(), oracle.heatmap_nms(y, k).numpy())
+
+
+def test_saturated_sigmoid_ties_are_peaks():
+    """NMS compares sigmoid values: neighbours that saturate to 1.0 are all peaks (decode.py:252)."""
+    import tauv_vision_amd as tv
+    logits = torch.full((1, 1, 8, 8), -5.0)
+    logits[0, 0, 3, 3] = 30.0
+    logits[0, 0, 3, 4] = 40.0   # sigmoid(30) == sigmoid(40) == 1.0 in fp32
+    ref = oracle.heatmap_nms(torch.sigmoid(logits), 3)
+    got = tv.heatmap_nms(torch.sigmoid(logits).cuda(), 3).cpu()
+    assert torch.equal(got, ref) and int((ref == 1.0).sum()) == 2

@@ -1,0 +1,176 @@
+"""GPU parity of the native CenterNet forward against the reference's golden outputs.
+
+fp32 mode (exact-f32 MFMA; BN folded at load): every Prediction tensor within
+1e-4 * max(1, |ref|max) of the reference PyTorch-CPU output. fp16 / bf16 modes are the
+throughput modes; their tolerance is stated per test (relative to the tensor's range).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import golden, models_index, case_by_name, case_state_dict, case_input, case_flags, keypoint_owner
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ["heatmap", "keypoint_heatmap", "keypoint_affinity", "size", "offset", "roll_bin", "roll_offset",
+          "pitch_bin", "pitch_offset", "yaw_bin", "yaw_offset", "depth"]
+TOL = {"fp32": 1e-4, "fp16": 2e-2, "bf16": 1e-1}
+
+
+def build(name, precision):
+    import tauv_vision_amd as tv
+    case = case_by_name(name)
+    o = case["objects"]
+    A = tv.AngleConfig
+    cfgs = []
+    for i in range(o["n_labels"]):
+        kp = o.get("keypoints_per_label", 0)
+        cfgs.append(tv.ObjectConfig(f"o{i}", A(o.get("yaw", False), 1.0), A(o.get("pitch", False), 1.0),
+                                    A(o.get("roll", False), 1.0), o.get("depth", False), kp > 0,
+                                    [(0.0, 0.0, 0.0)] * kp if kp else None))
+    oc = tv.ObjectConfigSet(cfgs)
+    model = tv.Centernet(tv.DLABackbone(case["heights"], case["channels"], case["downsamples"]), oc,
+                         precision=precision)
+    model.load_state_dict(case_state_dict(name))
+    model = model.cuda().eval()
+    mc = tv.ModelConfig(case["heights"], case["channels"], case["in_h"], case["in_w"], case["downsamples"], 1.0)
+    return model, oc, mc, case
+
+
+def _cmp(pred, g, tol):
+    for f in FIELDS:
+        t = getattr(pred, f)
+        if f not in g.files:
+            assert t is None, f
+            continue
+        ref = g[f]
+        got = t.detach().cpu().numpy()
+        assert got.shape == ref.shape, (f, got.shape, ref.shape)
+        scale = max(1.0, float(np.abs(ref).max()))
+        err = float(np.abs(got - ref).max())
+        assert err <= tol * scale, f"{f}: max|err| {err:.3e} > {tol} * {scale:.3g}"
+
+
+SMALL = [n for n in models_index() if n != "r18_c128_b1_480x640"]
+
+
+@pytest.mark.parametrize("name", SMALL)
+def test_forward_fp32_matches_reference(name):
+    model, oc, mc, case = build(name, "fp32")
+    with torch.no_grad():
+        pred = model(case_input(name).cuda())
+    _cmp(pred, golden(f"model_{name}"), TOL["fp32"])
+
+
+def test_forward_fp32_full_size_r18():
+    """The BASELINE "R18" (Centernet+DLABackbone [2]*5/[128]*6, ds 2) at 480x640."""
+    name = "r18_c128_b1_480x640"
+    model, oc, mc, case = build(name, "fp32")
+    pred = model(case_input(name).cuda())
+    g = golden(f"model_{name}")
+    _cmp(pred, g, TOL["fp32"])
+    # end-to-end decode: same detections as the reference (K=20)
+    import tauv_vision_amd as tv
+    for thr in (0.05, 0.3):
+        got = tv.decode(pred, mc, 20, thr)
+        ref = g[f"decode_thr{thr}"]
+        for b in range(ref.shape[0]):
+            n = int(np.nansum(ref[b, :, 7]))
+            assert len(got[b]) == n
+            for i, d in enumerate(got[b]):
+                assert int(d.label) == int(ref[b, i, 0])
+                np.testing.assert_allclose([float(d.score), d.y, d.x, d.h, d.w], ref[b, i, 1:6], atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("name", ["r18_c16_b2_96x128", "square_c32_b2_128", "r18_c128_b1_480x640"])
+def test_forward_low_precision(name, precision):
+    model, oc, mc, case = build(name, precision)
+    pred = model(case_input(name).cuda())
+    _cmp(pred, golden(f"model_{name}"), TOL[precision])
+
+
+@pytest.mark.parametrize("name", ["r18_c16_b2_96x128", "torpedo_c16_b1_360x640"])
+def test_decode_on_network_output(name):
+    import tauv_vision_amd as tv
+    model, oc, mc, case = build(name, "fp32")
+    pred = model(case_input(name).cuda())
+    g = golden(f"model_{name}")
+    for thr in (0.05, 0.3):
+        got = tv.decode(pred, mc, 20, thr)
+        ref = g[f"decode_thr{thr}"]
+        for b in range(ref.shape[0]):
+            assert len(got[b]) == int(np.nansum(ref[b, :, 7]))
+            for i, d in enumerate(got[b]):
+                assert int(d.label) == int(ref[b, i, 0])
+                np.testing.assert_allclose([float(d.score), d.y, d.x, d.h, d.w], ref[b, i, 1:6], atol=1e-4, rtol=1e-4)
+    if "decode_keypoints" in g.files:
+        kd = tv.decode_keypoints(pred, mc, oc, np.eye(3), 10, 50, 0.05, 0.05, 0.3)
+        ref = g["decode_keypoints"]
+        for b in range(ref.shape[0]):
+            assert len(kd[b]) == int(np.nansum(ref[b, :, 6]))
+            for i, d in enumerate(kd[b]):
+                row = [d.label, d.score, d.y, d.x, d.h, d.w, 1.0]
+                for j in range(len(d.keypoints)):
+                    row += ([np.nan] * 5 if d.keypoints[j] is None else
+                            [*d.keypoints[j], d.keypoint_scores[j], *d.keypoint_affinities[j]])
+                np.testing.assert_allclose(np.array(row, dtype=np.float64), ref[b, i], atol=1e-4, rtol=1e-4)
+
+
+def test_u8_frames_path_matches_normalized_input():
+    """forward_frames(u8) == forward(Normalize(ToTensor(u8))) (centernet_node.py:90-92)."""
+    from recipe import seeded_u8_frames, normalize
+    model, oc, mc, case = build("r18_c16_b2_96x128", "fp32")
+    fr = seeded_u8_frames(3, 96, 128, seed=7)
+    img = normalize(fr.permute(0, 3, 1, 2).float() / 255.0)
+    a = model(img.cuda())
+    b = model.forward_frames(fr.cuda())
+    assert torch.equal(a.heatmap.cpu(), b.heatmap.cpu())
+    assert torch.equal(a.size.cpu(), b.size.cpu())
+
+
+def test_batch_independence_and_determinism():
+    """Frames are independent: a batch equals its frames run one by one (bit-exact), and
+    repeated runs are bit-identical."""
+    model, oc, mc, case = build("r18_c16_b2_96x128", "fp16")
+    from recipe import seeded_u8_frames, normalize
+    img = normalize(seeded_u8_frames(5, 96, 128, seed=9).permute(0, 3, 1, 2).float() / 255.0).cuda()
+    full = model(img).heatmap.cpu()
+    for i in range(5):
+        one = model(img[i:i + 1]).heatmap.cpu()
+        assert torch.equal(one[0], full[i])
+    assert torch.equal(model(img).heatmap.cpu(), full)
+
+
+def test_concurrent_streams():
+    """Engine is immutable after create; two streams forward concurrently with their own
+    workspaces (rospy runs one callback thread per camera, centernet_node.py:58-65)."""
+    import threading
+    model, oc, mc, case = build("r18_c16_b2_96x128", "fp32")
+    img = case_input("r18_c16_b2_96x128").cuda()
+    ref = model(img).heatmap.cpu()
+    results = [None, None]
+
+    def run(i):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            outs = [model(img).heatmap.clone() for _ in range(3)]
+        s.synchronize()
+        results[i] = [o.cpu() for o in outs]
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    for r in results:
+        for o in r:
+            assert torch.equal(o, ref)
+
+
+def test_large_batch_property_fp16():
+    """B=64 at 480x640 (the bench workload): identical frames give identical outputs and
+    match the B=1 run bit-exactly (size-independent property at full size)."""
+    model, oc, mc, case = build("r18_c128_b1_480x640", "fp16")
+    img = case_input("r18_c128_b1_480x640").cuda()
+    one = model(img).heatmap
+    many = model(img.expand(64, -1, -1, -1).contiguous()).heatmap
+    assert torch.equal(many, one.expand(64, -1, -1, -1))

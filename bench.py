@@ -199,7 +199,7 @@ def main():
                 p1.step(f1)
         torch.cuda.current_stream(device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, stream=s):
             p1.step(f1)
         for _ in range(10):
             graph.replay()

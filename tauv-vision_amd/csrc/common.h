@@ -36,6 +36,17 @@ struct ConvSegment {
 
 constexpr int kMaxSeg = 8;
 
+// Host-precomputed descriptor of one 128-byte k-step of the pipelined kernel: which source
+// tensor and which tap/channel window it reads (one scalar load per k-step in the kernel).
+struct KStep {
+  const void* src;
+  int ky, kx, c0;            // uniform mode: the k-step lies in tap (ky, kx), channels [c0, c0+BK)
+  int H, W, ldc, stride, pad;
+  int mode;                  // 0: uniform tap; 1: per-lane taps (C = 1 << cshift < BK)
+  int cshift, kw, ntaps, tap0;
+  float kw_inv;              // 1 / kw: per-lane ky = floor((tap + 0.5) * kw_inv), exact for small taps
+};
+
 struct ConvParams {
   ConvSegment seg[kMaxSeg];
   int nseg;
@@ -54,7 +65,15 @@ struct ConvParams {
   int tH, tW, sy, sx;   // target grid and (row, col) shift
   const void* add;      // tensor added at the target pixel (compute dtype)
   int add_ldc;
+  const void* zero;     // >= 16 zero bytes: source of padding taps for LDS-DMA loads
+  const KStep* ks;      // pipelined kernel: one descriptor per k-step (nks of them)
+  int nks;
 };
+
+// Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
+int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
+                     hipStream_t s);
+constexpr int kPipeTileM = 256;
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,

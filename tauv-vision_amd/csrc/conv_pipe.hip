@@ -1,0 +1,307 @@
+// Pipelined implicit-GEMM convolution for large layers (gfx950).
+//
+// Same GEMM view and epilogues as conv.hip (rows = NHWC output pixels, columns = output
+// channels, K = taps x channels), restructured for MI355X's memory system:
+//   * 256-pixel x 128-channel tile per 512-thread workgroup (8 waves = 2 per SIMD, each
+//     wave a 64x64 sub-tile of 2x2 v_mfma_f32_32x32x16 / 32x32x2f32 tiles);
+//   * operands move global -> LDS by LDS-DMA (global_load_lds_dwordx4), no staging VGPRs:
+//     one wave-instruction fills 1 KiB = 8 rows x 128 B; the XOR bank swizzle is applied to
+//     the per-lane SOURCE address (the LDS image is lane-linear); padding taps read a
+//     zero page instead of being masked;
+//   * a 3-slot LDS ring (48 KiB per k-step) with one raw s_barrier per k-step and a counted
+//     `s_waitcnt vmcnt`, so two k-steps of DMA stay in flight under the MFMAs;
+//   * fragment reads are inline-asm ds_read_b128 (double-buffered per 16-deep sub-step) so
+//     the compiler does not insert a vmcnt(0) drain in front of LDS reads while DMA to
+//     other ring slots is in flight.
+#include "conv_common.h"
+
+namespace tv {
+namespace pipe {
+
+constexpr int BM = 256, BN = 128, NT = 512, NW = NT / 64, S = 3;
+constexpr int ROWB = 128;                    // bytes of K per k-step per row
+constexpr int A_BYTES = BM * ROWB;           // 32 KiB
+constexpr int B_BYTES = BN * ROWB;           // 16 KiB
+constexpr int STAGE = A_BYTES + B_BYTES;     // 48 KiB
+constexpr int RING = S * STAGE;              // 144 KiB
+constexpr int EROW = BN * 4 + 16;            // fp32 epilogue row (bytes)
+constexpr int LDS = RING > BM * EROW ? RING : BM * EROW;
+constexpr int GA = BM / 8 / NW;              // A pieces (1 KiB) per wave per k-step = 4
+constexpr int GB = BN / 8 / NW;              // B pieces per wave per k-step = 2
+constexpr int G = GA + GB;                   // LDS-DMA instructions per wave per k-step
+
+typedef __attribute__((address_space(3))) char lds_char;
+typedef const __attribute__((address_space(1))) void gvoid;
+
+__device__ __forceinline__ void dma16(const void* src, lds_char* dst_wave_base) {
+  __builtin_amdgcn_global_load_lds((gvoid*)src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ u32x4 ds_read16(unsigned addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ u32x4 ds_read16_off(unsigned addr) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+  return v;
+}
+
+__device__ __forceinline__ uint4 to_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+
+template <typename T, typename OutT, int MODE>
+__global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict__ pp, void* out_ptr) {
+  const ConvParams& p = *pp;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int BK = ROWB / sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  lds_char* lds = (lds_char*)smem;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): LDS-DMA base in M0
+
+  const int nb = p.mtiles * p.ntiles;
+  const int bid = blockIdx.x;
+  const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int ntile = lin % p.ntiles;
+  const int mtile = lin / p.ntiles;
+  const int m0 = mtile * BM;
+  const int n0 = ntile * BN;
+
+  // ---- DMA geometry. A piece i of this wave covers tile rows (wave*GA + i)*8 + lane/8; the
+  // lane's LDS slot is lane%8 and it fetches chunk (lane%8) ^ ((row>>1)&7) of that row.
+  int pb[GA], poy[GA], pox[GA], pc[GA];
+  bool pv[GA];
+  const int hw = p.Ho * p.Wo;
+#pragma unroll
+  for (int i = 0; i < GA; ++i) {
+    const int row = (wave * GA + i) * 8 + (lane >> 3);
+    const int m = m0 + row;
+    pv[i] = m < p.M;
+    const int mm = pv[i] ? m : 0;
+    pb[i] = mm / hw;
+    const int rem = mm - pb[i] * hw;
+    poy[i] = rem / p.Wo;
+    pox[i] = rem - poy[i] * p.Wo;
+    pc[i] = (lane & 7) ^ ((row >> 1) & 7);
+  }
+  const T* wsrc[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) {
+    const int row = (wave * GB + i) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    wsrc[i] = reinterpret_cast<const T*>(p.weight) + (size_t)(n0 + row) * p.Kpad + c * VEC;
+  }
+  const int total_ks = p.nks;
+  const void* const zero = p.zero;  // hoisted: the DMA intrinsic is treated as a memory clobber
+  // constant address space: the per-k-step descriptor read is a scalar load, not a
+  // (vmcnt-counted) vector load that would drain the DMA pipeline
+  const __attribute__((address_space(4))) KStep* kdesc = (const __attribute__((address_space(4))) KStep*)p.ks;
+
+  auto issue = [&](int ks, int slot) __attribute__((always_inline)) {
+    // wave-uniform descriptor: 64 bytes by scalar loads (constant address space)
+    const __attribute__((address_space(4))) u32x4* kq = (const __attribute__((address_space(4))) u32x4*)(kdesc + ks);
+    struct { u32x4 q[4]; } raw = {{kq[0], kq[1], kq[2], kq[3]}};
+    const KStep d = __builtin_bit_cast(KStep, raw);
+    const T* src = reinterpret_cast<const T*>(d.src);
+    lds_char* abase = lds + slot * STAGE + wave * GA * 1024;
+    if (d.mode == 0) {
+      // the whole k-step lies in one tap (ky, kx), channels [c0, c0 + BK)
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const int iy = poy[i] * d.stride + d.ky - d.pad;
+        const int ix = pox[i] * d.stride + d.kx - d.pad;
+        const bool ok = pv[i] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const void* a = ok ? (const void*)(src + ((size_t)(pb[i] * d.H + iy) * d.W + ix) * d.ldc + d.c0 + pc[i] * VEC)
+                           : zero;
+        dma16(a, abase + i * 1024);
+      }
+    } else {
+      // small C (a power of two below BK): each 16-byte chunk is its own tap
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const int ke = pc[i] * VEC;
+        const int tap = d.tap0 + (ke >> d.cshift);
+        const int ci = ke & ((1 << d.cshift) - 1);
+        const int ky = (int)(((float)tap + 0.5f) * d.kw_inv);
+        const int kx = tap - ky * d.kw;
+        const int iy = poy[i] * d.stride + ky - d.pad;
+        const int ix = pox[i] * d.stride + kx - d.pad;
+        const bool ok = pv[i] && tap < d.ntaps && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const void* a = ok ? (const void*)(src + ((size_t)(pb[i] * d.H + iy) * d.W + ix) * d.ldc + ci) : zero;
+        dma16(a, abase + i * 1024);
+      }
+    }
+    lds_char* bbase = lds + slot * STAGE + A_BYTES + wave * GB * 1024;
+#pragma unroll
+    for (int i = 0; i < GB; ++i) dma16(wsrc[i] + (size_t)ks * BK, bbase + i * 1024);
+  };
+
+  // ---- MFMA geometry: wave (wm, wn) owns pixels [wm*64,+64) x channels [wn*64,+64)
+  const int wm = wave & 3;
+  const int wn = wave >> 2;
+  const int lrow = lane & 31;
+  const int lh = lane >> 5;
+  const int xr = wm * 64 + lrow;   // pixel row of fragment t=0 (t=1 at +32 rows = +4096 B)
+  const int wr = wn * 64 + lrow;   // weight row
+  unsigned xaddr[4], waddr[4];
+  const unsigned lds0 = (unsigned)(uintptr_t)lds;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = 2 * j + lh;
+    xaddr[j] = lds0 + xr * ROWB + ((c ^ ((xr >> 1) & 7)) << 4);
+    waddr[j] = lds0 + A_BYTES + wr * ROWB + ((c ^ ((wr >> 1) & 7)) << 4);
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < total_ks) issue(s, s);
+
+  for (int ks = 0; ks < total_ks; ++ks) {
+    if (ks + 1 < total_ks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (S - 2)) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + S - 1 < total_ks) issue(ks + S - 1, (ks + S - 1) % S);
+    const unsigned so = (unsigned)((ks % S) * STAGE);
+    u32x4 fw[2][2], fx[2][2];
+    fw[0][0] = ds_read16(waddr[0] + so);
+    fw[0][1] = ds_read16_off<32 * ROWB>(waddr[0] + so);
+    fx[0][0] = ds_read16(xaddr[0] + so);
+    fx[0][1] = ds_read16_off<32 * ROWB>(xaddr[0] + so);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cb = j & 1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (j < 3) {
+        fw[cb ^ 1][0] = ds_read16(waddr[j + 1] + so);
+        fw[cb ^ 1][1] = ds_read16_off<32 * ROWB>(waddr[j + 1] + so);
+        fx[cb ^ 1][0] = ds_read16(xaddr[j + 1] + so);
+        fx[cb ^ 1][1] = ds_read16_off<32 * ROWB>(xaddr[j + 1] + so);
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) Mfma<T>::run(to_u4(fw[cb][a]), to_u4(fx[cb][b]), acc[a][b]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // ---- epilogue: bias + activation into an fp32 staging tile, then 16-byte stores
+  __syncthreads();
+  float* stg = reinterpret_cast<float*>(smem);
+  constexpr int SR = EROW / 4;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int pix = wm * 64 + b * 32 + lrow;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ch = wn * 64 + a * 32 + 8 * g + 4 * lh;
+        const uint4 braw = gload16(p.bias + n0 + ch);
+        const float bias4[4] = {__uint_as_float(braw.x), __uint_as_float(braw.y), __uint_as_float(braw.z),
+                                __uint_as_float(braw.w)};
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = acc[a][b][4 * g + e] + bias4[e];
+          if (p.act == 1) x = fmaxf(x, 0.0f);
+          else if (p.act == 2) x = x >= 0.0f ? x : 0.01f * x;
+          v[e] = x;
+        }
+        *reinterpret_cast<f32x4*>(stg + pix * SR + ch) = f32x4{v[0], v[1], v[2], v[3]};
+      }
+    }
+  }
+  __syncthreads();
+
+  constexpr int OVEC = 16 / sizeof(OutT);
+  constexpr int CPR = BN / OVEC;
+  for (int qd = tid; qd < BM * CPR; qd += NT) {
+    const int row = qd / CPR;
+    const int cc = qd - row * CPR;
+    const int m = m0 + row;
+    const int n = n0 + cc * OVEC;
+    if (m >= p.M || n >= p.N) continue;
+    const float* sv = stg + row * SR + cc * OVEC;
+    if (MODE == 0) {
+      OutT* dst = reinterpret_cast<OutT*>(out_ptr) + (size_t)m * p.out_ldc + p.out_coff + n;
+      store_chunk<OutT>(dst, sv);
+    } else {
+      const int b = m / hw;
+      const int rem = m - b * hw;
+      const int oy = rem / p.Wo;
+      const int ox = rem - oy * p.Wo;
+      const int phase = n / p.up_cout;
+      const int co = n - phase * p.up_cout;
+      const int Y = oy * p.up_s + phase / p.up_s + p.sy;
+      const int X = ox * p.up_s + phase % p.up_s + p.sx;
+      if (Y >= p.tH || X >= p.tW) continue;
+      const size_t tpix = (size_t)(b * p.tH + Y) * p.tW + X;
+      const T* ad = reinterpret_cast<const T*>(p.add) + tpix * p.add_ldc + co;
+      const uint4 raw = gload16(ad);
+      const uint32_t rw4[4] = {raw.x, raw.y, raw.z, raw.w};
+      float v[OVEC];
+      if constexpr (sizeof(T) == 4) {
+#pragma unroll
+        for (int e = 0; e < OVEC; ++e) v[e] = __uint_as_float(rw4[e]) + sv[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < OVEC; ++e) {
+          const uint16_t bits = (uint16_t)(rw4[e >> 1] >> (16 * (e & 1)));
+          v[e] = to_f(__builtin_bit_cast(T, bits)) + sv[e];
+        }
+      }
+      OutT* dst = reinterpret_cast<OutT*>(out_ptr) + tpix * p.out_ldc + co;
+      store_chunk<OutT>(dst, v);
+    }
+  }
+}
+
+template <typename T, typename OutT, int MODE>
+static int launch_pipe_t(const ConvParams& p, const ConvParams* dp, void* out, hipStream_t s) {
+  auto k = conv_pipe<T, OutT, MODE>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    if (e != hipSuccess) {
+      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+      return 3;
+    }
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3(p.mtiles * p.ntiles), dim3(NT), LDS, s, dp, out);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace pipe
+
+int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
+                     hipStream_t s) {
+  using namespace pipe;
+  if (dtype == F32) {
+    return mode == 0 ? launch_pipe_t<float, float, 0>(p, dp, out, s) : launch_pipe_t<float, float, 1>(p, dp, out, s);
+  } else if (dtype == F16) {
+    if (mode == 1) return launch_pipe_t<_Float16, _Float16, 1>(p, dp, out, s);
+    return out_f32 ? launch_pipe_t<_Float16, float, 0>(p, dp, out, s)
+                   : launch_pipe_t<_Float16, _Float16, 0>(p, dp, out, s);
+  } else {
+    if (mode == 1) return launch_pipe_t<__bf16, __bf16, 1>(p, dp, out, s);
+    return out_f32 ? launch_pipe_t<__bf16, float, 0>(p, dp, out, s) : launch_pipe_t<__bf16, __bf16, 0>(p, dp, out, s);
+  }
+}
+
+}  // namespace tv

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <set>
 
 namespace tv {
@@ -189,6 +190,9 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     host_w[w[i].name] = {w[i].data, w[i].numel};
   }
   TV_HIP(hipSetDevice(device));
+  TV_HIP(hipMalloc(&zero_page, 256));
+  TV_HIP(hipMemset(zero_page, 0, 256));
+  if (const char* env = std::getenv("TV_CONV_PIPE")) pipe_mode = std::atoi(env);
   packed.resize(plan.ops.size());
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     rc = pack_op(i);
@@ -199,6 +203,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
 }
 
 Engine::~Engine() {
+  if (zero_page) (void)hipFree(zero_page);
   for (auto& p : packed) {
     if (p.w) (void)hipFree(p.w);
     if (p.bias) (void)hipFree(p.bias);
@@ -206,6 +211,7 @@ Engine::~Engine() {
   for (auto& kv : workspaces) {
     if (kv.second->arena) (void)hipFree(kv.second->arena);
     if (kv.second->dparams) (void)hipFree(kv.second->dparams);
+    if (kv.second->dks) (void)hipFree(kv.second->dks);
     delete kv.second;
   }
 }
@@ -306,6 +312,55 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.add_ldc = plan.tensors[op.add].C;
     }
   }
+  // k-step descriptors for the pipelined kernel and the per-op kernel choice
+  const int BK = 128 / esz;
+  std::vector<KStep> all_ks;
+  std::vector<size_t> ks_off(plan.ops.size(), 0);
+  ws->use_pipe.assign(plan.ops.size(), 0);
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    if (op.kind == OP_PREP) continue;
+    ConvParams& p = ws->params[i];
+    std::vector<KStep> ks;
+    bool ok = true;
+    for (int s = 0; s < p.nseg && ok; ++s) {
+      const ConvSegment& sg = p.seg[s];
+      for (int kk = 0; kk < sg.ksteps; ++kk) {
+        KStep d{};
+        d.src = sg.src;
+        d.H = sg.H; d.W = sg.W; d.ldc = sg.ldc; d.stride = sg.stride; d.pad = sg.pad;
+        d.kw = sg.kw; d.ntaps = sg.kh * sg.kw; d.kw_inv = 1.0f / (float)sg.kw;
+        const int kel = kk * BK;
+        if (sg.C % BK == 0) {
+          const int tap = kel / sg.C;
+          d.mode = 0; d.ky = tap / sg.kw; d.kx = tap % sg.kw; d.c0 = kel % sg.C;
+        } else if (sg.C < BK && (sg.C & (sg.C - 1)) == 0 && d.ntaps + BK / sg.C < 4096) {
+          d.mode = 1; d.tap0 = kel / sg.C;
+          while ((1 << d.cshift) < sg.C) ++d.cshift;
+        } else {
+          ok = false;
+          break;
+        }
+        ks.push_back(d);
+      }
+    }
+    const int mt = (p.M + kPipeTileM - 1) / kPipeTileM;
+    const bool big = (long)mt * p.ntiles >= 256;
+    ws->use_pipe[i] = ok && (pipe_mode == 1 || (pipe_mode < 0 && big));
+    if (ws->use_pipe[i]) {
+      ks_off[i] = all_ks.size();
+      all_ks.insert(all_ks.end(), ks.begin(), ks.end());
+      p.nks = (int)ks.size();
+      p.mtiles = mt;
+    }
+    p.zero = zero_page;
+  }
+  if (!all_ks.empty()) {
+    TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
+    TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
+    for (size_t i = 0; i < plan.ops.size(); ++i)
+      if (ws->use_pipe[i]) ws->params[i].ks = ws->dks + ks_off[i];
+  }
   TV_HIP(hipMalloc((void**)&ws->dparams, ws->params.size() * sizeof(ConvParams)));
   TV_HIP(hipMemcpy(ws->dparams, ws->params.data(), ws->params.size() * sizeof(ConvParams), hipMemcpyHostToDevice));
   return TV_OK;
@@ -324,6 +379,7 @@ int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
   if (rc) {
     if (ws->arena) (void)hipFree(ws->arena);
     if (ws->dparams) (void)hipFree(ws->dparams);
+    if (ws->dks) (void)hipFree(ws->dks);
     delete ws;
     return rc;
   }
@@ -343,7 +399,9 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   ConvParams p = ws->params[i];
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
-  int rc = launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, op.kind == OP_CONVT_ADD ? 1 : 0, s);
+  const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
+  int rc = ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
+                           : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
   if (rc) return rc;
   if (op.kind == OP_CONVT_ADD) {
     const TensorSpec& tgt = plan.tensors[op.out];

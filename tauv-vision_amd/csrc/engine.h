@@ -25,6 +25,8 @@ struct Workspace {
   std::vector<size_t> off;          // per tensor
   std::vector<ConvParams> params;   // per op (host copy)
   ConvParams* dparams = nullptr;    // per op (device copy)
+  std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
+  KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
 };
 
 struct Engine {
@@ -34,6 +36,8 @@ struct Engine {
   int dtype = F32;
   std::vector<Packed> packed;  // per op
   size_t weight_bytes = 0;
+  void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
+  int pipe_mode = -1;          // -1 auto, 0 never, 1 whenever representable (env TV_CONV_PIPE)
   std::mutex mu;
   std::map<std::pair<void*, int>, Workspace*> workspaces;
   std::unordered_map<std::string, std::pair<const float*, int64_t>> host_w;  // during create only

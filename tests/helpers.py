@@ -36,7 +36,8 @@ def case_state_dict(name):
     checks = golden(f"model_{name}")["weight_checksums"]
     got = np.array([[float(v.double().sum()), float(v.double().abs().sum())]
                     if v.dtype.is_floating_point else [float(v), 0.0] for v in sd.values()])
-    assert np.array_equal(got, checks), "seeded weight recipe drifted from the golden run"
+    # double sums of large tensors depend on the host's reduction threading: compare to 1e-10
+    assert np.allclose(got, checks, rtol=1e-10, atol=1e-12), "seeded weight recipe drifted from the golden run"
     return sd
 
 
@@ -44,7 +45,8 @@ def case_input(name):
     case = case_by_name(name)
     img = seeded_input(case)
     chk = golden(f"model_{name}")["img_checksum"]
-    assert float(img.double().sum()) == chk[0] and float(img.double().abs().sum()) == chk[1]
+    got = [float(img.double().sum()), float(img.double().abs().sum())]
+    assert np.allclose(got, chk, rtol=1e-10, atol=1e-9), "seeded input drifted from the golden run"
     return img
 
 

@@ -82,6 +82,9 @@ def conv_roofline(pipe, frames_f32, precision, reps=3):
         else:
             for b, o in zip(best, ops):
                 b[1] = min(b[1], o[1])
+    if os.environ.get("TV_PROFILE_OUT"):
+        with open(os.environ["TV_PROFILE_OUT"], "w") as f:
+            json.dump([{"op": o[0], "ms": o[1], "gflop": o[2] / 1e9} for o in best], f, indent=0)
     conv = [o for o in best if o[2] > 0]
     ms = sum(o[1] for o in conv)
     flops = sum(o[2] for o in conv)

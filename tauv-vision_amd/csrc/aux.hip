@@ -1,7 +1,7 @@
 // Memory-bound helper kernels around the conv stack (gfx950).
 //  * input staging: NCHW fp32 (Centernet.forward's contract, centernet.py:65) or raw u8 HWC
 //    frames with the node's ToTensor + Normalize(ImageNet) fused (centernet_node.py:90-92),
-//    written as NHWC with channels zero-padded to one 16-byte chunk per pixel;
+//    written row-expanded for the 7x7 stem (7 horizontal taps x 3 channels per pixel);
 //  * the pad_to_match margin: target pixels that the shifted upsample does not cover get the
 //    skip tensor alone (dla.py:205-207 zero padding).
 #include "common.h"
@@ -11,38 +11,61 @@ namespace tv {
 __constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
 __constant__ float kStd[3] = {0.229f, 0.224f, 0.225f};
 
+// Row-expanded staging for the 7x7 stem (see planner.cpp): output pixel (y, x) holds
+// [kx*3 + c] = input(y, x + kx - 3, c) for kx < 7 (zero outside the image), then zeros up to
+// `cpad` (a whole number of 16-byte chunks). One thread per output pixel.
 template <typename T>
-__device__ __forceinline__ void write_pixel(T* dst, float r, float g, float b) {
-  constexpr int V = 16 / sizeof(T);
-  T t[V];
+__device__ __forceinline__ void write_expanded(T* dst, const float (&v)[7][3], int cpad) {
+  T t[24];
 #pragma unroll
-  for (int e = 0; e < V; ++e) t[e] = (T)0.0f;
-  t[0] = (T)r;
-  t[1] = (T)g;
-  t[2] = (T)b;
-  *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(t);
+  for (int k = 0; k < 7; ++k)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) t[k * 3 + c] = (T)v[k][c];
+#pragma unroll
+  for (int j = 21; j < 24; ++j) t[j] = (T)0.0f;
+  const uint4* src = reinterpret_cast<const uint4*>(t);
+  uint4* out = reinterpret_cast<uint4*>(dst);
+  const int chunks = cpad * (int)sizeof(T) / 16;
+#pragma unroll
+  for (int q = 0; q < 24 * (int)sizeof(T) / 16; ++q)
+    if (q < chunks) out[q] = src[q];
 }
 
 template <typename T>
-__global__ void prep_nchw(const float* __restrict__ img, int B, int HW, T* __restrict__ out) {
+__global__ void prep_nchw(const float* __restrict__ img, int B, int H, int W, int cpad, T* __restrict__ out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t HW = (size_t)H * W;
   if (i >= (size_t)B * HW) return;
-  size_t b = i / HW, px = i - b * HW;
-  const float* base = img + b * 3 * HW + px;
-  constexpr int V = 16 / sizeof(T);
-  write_pixel<T>(out + i * V, base[0], base[HW], base[2 * HW]);
+  const size_t b = i / HW, px = i - b * HW;
+  const int x = px % W;
+  const float* base = img + b * 3 * HW + (px - x);
+  float v[7][3];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int xx = x + k - 3;
+    const bool ok = xx >= 0 && xx < W;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[k][c] = ok ? base[c * HW + xx] : 0.0f;
+  }
+  write_expanded<T>(out + i * cpad, v, cpad);
 }
 
 template <typename T>
-__global__ void prep_u8(const uint8_t* __restrict__ fr, size_t npix, T* __restrict__ out) {
+__global__ void prep_u8(const uint8_t* __restrict__ fr, int B, int H, int W, int cpad, T* __restrict__ out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= npix) return;
-  const uint8_t* p = fr + i * 3;
-  float v[3];
+  const size_t HW = (size_t)H * W;
+  if (i >= (size_t)B * HW) return;
+  const int x = (i % HW) % W;
+  const uint8_t* row = fr + (i - x) * 3;
+  float v[7][3];
 #pragma unroll
-  for (int c = 0; c < 3; ++c) v[c] = ((float)p[c] / 255.0f - kMean[c]) / kStd[c];
-  constexpr int V = 16 / sizeof(T);
-  write_pixel<T>(out + i * V, v[0], v[1], v[2]);
+  for (int k = 0; k < 7; ++k) {
+    const int xx = x + k - 3;
+    const bool ok = xx >= 0 && xx < W;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[k][c] = ok ? ((float)row[xx * 3 + c] / 255.0f - kMean[c]) / kStd[c] : 0.0f;
+  }
+  write_expanded<T>(out + i * cpad, v, cpad);
 }
 
 template <typename F>
@@ -53,22 +76,22 @@ static int dispatch_dtype(int dtype, F&& f) {
 }
 
 int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad, int dtype, hipStream_t s) {
-  if (cpad * dtype_size(dtype) != 16) { set_error("prep: pixel must be one 16-byte chunk"); return 1; }
+  if (cpad != 24) { set_error("prep: row-expanded stem input must have 24 channels"); return 1; }
   size_t n = (size_t)B * H * W;
   return dispatch_dtype(dtype, [&](auto tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
-    hipLaunchKernelGGL(prep_nchw<T>, dim3((n + 255) / 256), dim3(256), 0, s, img, B, H * W, (T*)out);
+    hipLaunchKernelGGL(prep_nchw<T>, dim3((n + 255) / 256), dim3(256), 0, s, img, B, H, W, cpad, (T*)out);
     TV_HIP(hipGetLastError());
     return 0;
   });
 }
 
 int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cpad, int dtype, hipStream_t s) {
-  if (cpad * dtype_size(dtype) != 16) { set_error("prep: pixel must be one 16-byte chunk"); return 1; }
+  if (cpad != 24) { set_error("prep: row-expanded stem input must have 24 channels"); return 1; }
   size_t n = (size_t)B * H * W;
   return dispatch_dtype(dtype, [&](auto tag) {
     using T = std::remove_pointer_t<decltype(tag)>;
-    hipLaunchKernelGGL(prep_u8<T>, dim3((n + 255) / 256), dim3(256), 0, s, frames, n, (T*)out);
+    hipLaunchKernelGGL(prep_u8<T>, dim3((n + 255) / 256), dim3(256), 0, s, frames, B, H, W, cpad, (T*)out);
     TV_HIP(hipGetLastError());
     return 0;
   });

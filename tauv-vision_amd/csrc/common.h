@@ -29,7 +29,7 @@ void set_error(const std::string& msg);
 struct ConvSegment {
   const void* src;  // element (b,y,x,c) at ((b*H + y)*W + x)*ldc + c
   int H, W, C, ldc;
-  int kh, kw, stride, pad;
+  int kh, kw, stride, pad, pad_w;
   int ksteps;  // ceil(kh*kw*C / BK); BK = 128 bytes of elements
   int kbase;   // first k-step of this segment in the packed weight rows
 };
@@ -40,12 +40,13 @@ constexpr int kMaxSeg = 8;
 // tensor and which tap/channel window it reads (one scalar load per k-step in the kernel).
 struct KStep {
   const void* src;
-  int ky, kx, c0;            // uniform mode: the k-step lies in tap (ky, kx), channels [c0, c0+BK)
-  int H, W, ldc, stride, pad;
-  int mode;                  // 0: uniform tap; 1: per-lane taps (C = 1 << cshift < BK)
-  int cshift, kw, ntaps, tap0;
-  float kw_inv;              // 1 / kw: per-lane ky = floor((tap + 0.5) * kw_inv), exact for small taps
+  long long off;             // mode 0: element offset of (tap, c0) from the lane's segment base pixel
+  int seg, tap, mode;        // mode 0: the k-step lies in one tap; 1: per-lane taps (C < BK)
+  int H, W, ldc, stride, pad_h, pad_w, kh, kw;
+  int q0, cpt;               // mode 1: first 16-byte chunk (within the segment's K), chunks per tap
+  float cpt_inv, kw_inv;     // mode 1: reciprocals for exact small-integer division
 };
+static_assert(sizeof(KStep) == 80, "KStep layout");
 
 struct ConvParams {
   ConvSegment seg[kMaxSeg];
@@ -68,12 +69,19 @@ struct ConvParams {
   const void* zero;     // >= 16 zero bytes: source of padding taps for LDS-DMA loads
   const KStep* ks;      // pipelined kernel: one descriptor per k-step (nks of them)
   int nks;
+  int ablate;           // timing experiments only (env TV_ABLATE): 1 no main-loop DMA, 2 no MFMA
 };
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
 int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
                      hipStream_t s);
 constexpr int kPipeTileM = 256;
+
+// Halo-tile 3x3 / stride 1 / pad 1 variant (conv_halo.hip): 256-pixel blocks of tw columns
+// (tw = 16 or 32); ConvParams.mtiles must be halo_tiles(B, H, W, tw).
+int launch_conv_halo(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int tw,
+                     hipStream_t s);
+int halo_tiles(int B, int H, int W, int tw);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,

@@ -45,7 +45,7 @@ __device__ __forceinline__ void load_tile(const ConvParams& p, int ks, int lc, c
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     int iy = poy[i] * sg.stride + ky - sg.pad;
-    int ix = pox[i] * sg.stride + kx - sg.pad;
+    int ix = pox[i] * sg.stride + kx - sg.pad_w;
     bool ok = pvalid[i] && tap_ok && iy >= 0 && iy < sg.H && ix >= 0 && ix < sg.W;
     iy = min(max(iy, 0), sg.H - 1);
     ix = min(max(ix, 0), sg.W - 1);

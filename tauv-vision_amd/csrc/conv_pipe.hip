@@ -102,43 +102,68 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   // (vmcnt-counted) vector load that would drain the DMA pipeline
   const __attribute__((address_space(4))) KStep* kdesc = (const __attribute__((address_space(4))) KStep*)p.ks;
 
+  // Per-segment lane state for uniform-tap k-steps: the lane's base pointer (pixel
+  // (b, oy*stride - pad_h, ox*stride - pad_w), its chunk) and a bit mask of the taps that land
+  // inside the image. A k-step then costs one bit test and one 64-bit add per piece.
+  const T* lbase[GA];
+  uint32_t lmask[GA];
+  int cur_seg = -1;
+  // weights: uniform base advanced per k-step, per-lane 32-bit offsets
+  const T* wbase = reinterpret_cast<const T*>(p.weight) + (size_t)n0 * p.Kpad;
+  uint32_t woff[GB];
+#pragma unroll
+  for (int i = 0; i < GB; ++i) woff[i] = (uint32_t)(wsrc[i] - wbase);
+
   auto issue = [&](int ks, int slot) __attribute__((always_inline)) {
-    // wave-uniform descriptor: 64 bytes by scalar loads (constant address space)
+    // wave-uniform descriptor: 80 bytes by scalar loads (constant address space)
     const __attribute__((address_space(4))) u32x4* kq = (const __attribute__((address_space(4))) u32x4*)(kdesc + ks);
-    struct { u32x4 q[4]; } raw = {{kq[0], kq[1], kq[2], kq[3]}};
+    struct { u32x4 q[5]; } raw = {{kq[0], kq[1], kq[2], kq[3], kq[4]}};
     const KStep d = __builtin_bit_cast(KStep, raw);
     const T* src = reinterpret_cast<const T*>(d.src);
     lds_char* abase = lds + slot * STAGE + wave * GA * 1024;
     if (d.mode == 0) {
-      // the whole k-step lies in one tap (ky, kx), channels [c0, c0 + BK)
+      if (d.seg != cur_seg) {
+        cur_seg = d.seg;
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+          const int iy0 = poy[i] * d.stride - d.pad_h;
+          const int ix0 = pox[i] * d.stride - d.pad_w;
+          lbase[i] = src + ((long long)(pb[i] * d.H + iy0) * d.W + ix0) * d.ldc + pc[i] * VEC;
+          uint32_t mk = 0;
+          for (int ky = 0; ky < d.kh; ++ky) {
+            const bool rok = (unsigned)(iy0 + ky) < (unsigned)d.H;
+            for (int kx = 0; kx < d.kw; ++kx)
+              mk |= (uint32_t)(rok && (unsigned)(ix0 + kx) < (unsigned)d.W) << (ky * d.kw + kx);
+          }
+          lmask[i] = pv[i] ? mk : 0u;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < GA; ++i) {
-        const int iy = poy[i] * d.stride + d.ky - d.pad;
-        const int ix = pox[i] * d.stride + d.kx - d.pad;
-        const bool ok = pv[i] && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
-        const void* a = ok ? (const void*)(src + ((size_t)(pb[i] * d.H + iy) * d.W + ix) * d.ldc + d.c0 + pc[i] * VEC)
-                           : zero;
-        dma16(a, abase + i * 1024);
+        const bool ok = (lmask[i] >> d.tap) & 1u;
+        dma16(ok ? (const void*)(lbase[i] + d.off) : zero, abase + i * 1024);
       }
     } else {
-      // small C (a power of two below BK): each 16-byte chunk is its own tap
+      // C below BK: every 16-byte chunk resolves its own tap (cpt chunks per tap)
+      cur_seg = -1;
 #pragma unroll
       for (int i = 0; i < GA; ++i) {
-        const int ke = pc[i] * VEC;
-        const int tap = d.tap0 + (ke >> d.cshift);
-        const int ci = ke & ((1 << d.cshift) - 1);
+        const int q = d.q0 + pc[i];
+        const int tap = (int)(((float)q + 0.5f) * d.cpt_inv);
+        const int ci = (q - tap * d.cpt) * VEC;
         const int ky = (int)(((float)tap + 0.5f) * d.kw_inv);
         const int kx = tap - ky * d.kw;
-        const int iy = poy[i] * d.stride + ky - d.pad;
-        const int ix = pox[i] * d.stride + kx - d.pad;
-        const bool ok = pv[i] && tap < d.ntaps && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
+        const int iy = poy[i] * d.stride + ky - d.pad_h;
+        const int ix = pox[i] * d.stride + kx - d.pad_w;
+        const bool ok = pv[i] && tap < d.kh * d.kw && (unsigned)iy < (unsigned)d.H && (unsigned)ix < (unsigned)d.W;
         const void* a = ok ? (const void*)(src + ((size_t)(pb[i] * d.H + iy) * d.W + ix) * d.ldc + ci) : zero;
         dma16(a, abase + i * 1024);
       }
     }
     lds_char* bbase = lds + slot * STAGE + A_BYTES + wave * GB * 1024;
+    const T* wk = wbase + (size_t)ks * BK;
 #pragma unroll
-    for (int i = 0; i < GB; ++i) dma16(wsrc[i] + (size_t)ks * BK, bbase + i * 1024);
+    for (int i = 0; i < GB; ++i) dma16(wk + woff[i], bbase + i * 1024);
   };
 
   // ---- MFMA geometry: wave (wm, wn) owns pixels [wm*64,+64) x channels [wn*64,+64)
@@ -163,39 +188,54 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
 
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < total_ks) issue(s, s);
-
-  for (int ks = 0; ks < total_ks; ++ks) {
-    if (ks + 1 < total_ks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G * (S - 2)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (ks + S - 1 < total_ks) issue(ks + S - 1, (ks + S - 1) % S);
+  // Fragments of one k-step (per sub-step j: W rows t=0,1 then X rows t=0,1). Two register
+  // sets: the next k-step's fragments are read while this k-step's MFMAs run, so LDS latency
+  // never sits between an MFMA and its operands.
+  u32x4 fa[4][4], fb[4][4];
+  auto read_frags = [&](int ks, u32x4(&f)[4][4]) __attribute__((always_inline)) {
     const unsigned so = (unsigned)((ks % S) * STAGE);
-    u32x4 fw[2][2], fx[2][2];
-    fw[0][0] = ds_read16(waddr[0] + so);
-    fw[0][1] = ds_read16_off<32 * ROWB>(waddr[0] + so);
-    fx[0][0] = ds_read16(xaddr[0] + so);
-    fx[0][1] = ds_read16_off<32 * ROWB>(xaddr[0] + so);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int cb = j & 1;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if (j < 3) {
-        fw[cb ^ 1][0] = ds_read16(waddr[j + 1] + so);
-        fw[cb ^ 1][1] = ds_read16_off<32 * ROWB>(waddr[j + 1] + so);
-        fx[cb ^ 1][0] = ds_read16(xaddr[j + 1] + so);
-        fx[cb ^ 1][1] = ds_read16_off<32 * ROWB>(xaddr[j + 1] + so);
-      }
+      f[j][0] = ds_read16(waddr[j] + so);
+      f[j][1] = ds_read16_off<32 * ROWB>(waddr[j] + so);
+      f[j][2] = ds_read16(xaddr[j] + so);
+      f[j][3] = ds_read16_off<32 * ROWB>(xaddr[j] + so);
+    }
+  };
+  auto mfmas = [&](const u32x4(&f)[4][4]) __attribute__((always_inline)) {
+    if (p.ablate & 2) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) Mfma<T>::run(to_u4(fw[cb][a]), to_u4(fx[cb][b]), acc[a][b]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
+        for (int b = 0; b < 2; ++b) Mfma<T>::run(to_u4(f[j][a]), to_u4(f[j][2 + b]), acc[a][b]);
+  };
+  // one k-step: stage ks's fragments are in `cur`; DMA keeps stages ks+2, ks+3 in flight
+  auto step = [&](int ks, u32x4(&cur)[4][4], u32x4(&nxt)[4][4]) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage ks landed
+    if (ks + 2 < total_ks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");  // stage ks+1 landed
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave: stage ks+1 visible, slot ks%S released
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + S < total_ks && !(p.ablate & 1)) issue(ks + S, ks % S);
+    if (ks + 1 < total_ks) read_frags(ks + 1, nxt);
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(cur);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int npro = total_ks < S ? total_ks : S;
+  for (int s = 0; s < npro; ++s) issue(s, s);
+  if (npro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+  else if (npro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  read_frags(0, fa);
+  for (int ks = 0; ks < total_ks; ks += 2) {
+    step(ks, fa, fb);
+    if (ks + 1 < total_ks) step(ks + 1, fb, fa);
   }
 
   // ---- epilogue: bias + activation into an fp32 staging tile, then 16-byte stores
@@ -228,31 +268,49 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   __syncthreads();
 
   constexpr int OVEC = 16 / sizeof(OutT);
-  constexpr int CPR = BN / OVEC;
-  for (int qd = tid; qd < BM * CPR; qd += NT) {
-    const int row = qd / CPR;
-    const int cc = qd - row * CPR;
-    const int m = m0 + row;
-    const int n = n0 + cc * OVEC;
-    if (m >= p.M || n >= p.N) continue;
-    const float* sv = stg + row * SR + cc * OVEC;
-    if (MODE == 0) {
-      OutT* dst = reinterpret_cast<OutT*>(out_ptr) + (size_t)m * p.out_ldc + p.out_coff + n;
-      store_chunk<OutT>(dst, sv);
-    } else {
+  constexpr int CPR = BN / OVEC;       // 16-byte chunks per staged row
+  constexpr int RSTEP = NT / CPR;      // rows covered per pass; each thread keeps one chunk column
+  constexpr int NP = BM / RSTEP;       // passes
+  const int cc = tid % CPR;
+  const int r0 = tid / CPR;
+  const int n = n0 + cc * OVEC;
+  if (MODE == 0) {
+    if (n < p.N) {
+#pragma unroll 4
+      for (int k = 0; k < NP; ++k) {
+        const int row = r0 + k * RSTEP;
+        const int m = m0 + row;
+        if (m >= p.M) break;
+        OutT* dst = reinterpret_cast<OutT*>(out_ptr) + (size_t)m * p.out_ldc + p.out_coff + n;
+        store_chunk<OutT>(dst, stg + row * SR + cc * OVEC);
+      }
+    }
+  } else {
+    // ConvTranspose phase scatter + skip add: this thread's channel chunk fixes (phase, co);
+    // all skip-tensor loads of the thread are issued before any is consumed.
+    const int phase = n / p.up_cout;
+    const int co = n - phase * p.up_cout;
+    const int pi = phase / p.up_s, pj = phase - pi * p.up_s;
+    size_t toff[NP];
+    uint4 av[NP];
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      const int m = m0 + r0 + k * RSTEP;
       const int b = m / hw;
       const int rem = m - b * hw;
       const int oy = rem / p.Wo;
       const int ox = rem - oy * p.Wo;
-      const int phase = n / p.up_cout;
-      const int co = n - phase * p.up_cout;
-      const int Y = oy * p.up_s + phase / p.up_s + p.sy;
-      const int X = ox * p.up_s + phase % p.up_s + p.sx;
-      if (Y >= p.tH || X >= p.tW) continue;
-      const size_t tpix = (size_t)(b * p.tH + Y) * p.tW + X;
-      const T* ad = reinterpret_cast<const T*>(p.add) + tpix * p.add_ldc + co;
-      const uint4 raw = gload16(ad);
-      const uint32_t rw4[4] = {raw.x, raw.y, raw.z, raw.w};
+      const int Y = oy * p.up_s + pi + p.sy;
+      const int X = ox * p.up_s + pj + p.sx;
+      const bool ok = n < p.N && m < p.M && Y < p.tH && X < p.tW;
+      toff[k] = ok ? (size_t)(b * p.tH + Y) * p.tW + X : ~(size_t)0;
+      av[k] = ok ? gload16(reinterpret_cast<const T*>(p.add) + toff[k] * p.add_ldc + co) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NP; ++k) {
+      if (toff[k] == ~(size_t)0) continue;
+      const float* sv = stg + (r0 + k * RSTEP) * SR + cc * OVEC;
+      const uint32_t rw4[4] = {av[k].x, av[k].y, av[k].z, av[k].w};
       float v[OVEC];
       if constexpr (sizeof(T) == 4) {
 #pragma unroll
@@ -264,8 +322,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
           v[e] = to_f(__builtin_bit_cast(T, bits)) + sv[e];
         }
       }
-      OutT* dst = reinterpret_cast<OutT*>(out_ptr) + tpix * p.out_ldc + co;
-      store_chunk<OutT>(dst, v);
+      store_chunk<OutT>(reinterpret_cast<OutT*>(out_ptr) + toff[k] * p.out_ldc + co, v);
     }
   }
 }

@@ -148,7 +148,8 @@ int Engine::pack_op(size_t oi) {
         int wcin = 0;
         for (const SegSpec& o : op.segs)
           if (o.wname == sg.wname) wcin = std::max(wcin, o.ci0 + o.cin);
-        const int kk = sg.kh * sg.kw;
+        const int re = sg.row_expand;  // row-expanded input: K index = ky * cs + kx * cin + c
+        const int kk = re ? sg.kh * re : sg.kh * sg.kw;
         const float* w = weight(sg.wname + ".weight", (int64_t)N * wcin * kk);
         if (!w) return TV_ENOTFOUND;
         std::vector<double> scale, shift;
@@ -158,9 +159,11 @@ int Engine::pack_op(size_t oi) {
           for (int co = 0; co < N; ++co) bias[co] += (float)shift[co];
         for (int co = 0; co < N; ++co)
           for (int ci = 0; ci < sg.cin; ++ci)
-            for (int t = 0; t < kk; ++t)
-              hw[(size_t)co * pk.Kpad + (size_t)kb * BK + t * cs + ci] =
+            for (int t = 0; t < kk; ++t) {
+              const size_t k = re ? (size_t)(t / re) * cs + (t % re) * sg.cin + ci : (size_t)t * cs + ci;
+              hw[(size_t)co * pk.Kpad + (size_t)kb * BK + k] =
                   (float)((double)w[((size_t)co * wcin + sg.ci0 + ci) * kk + t] * scale[co]);
+            }
         kb += pk.seg_ksteps[si];
       }
     }
@@ -193,6 +196,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   TV_HIP(hipMalloc(&zero_page, 256));
   TV_HIP(hipMemset(zero_page, 0, 256));
   if (const char* env = std::getenv("TV_CONV_PIPE")) pipe_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
   packed.resize(plan.ops.size());
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     rc = pack_op(i);
@@ -275,7 +279,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
         const SegSpec& sg = op.segs[s];
         const TensorSpec& t = plan.tensors[sg.src];
         p.seg[s] = ConvSegment{base + ws->off[sg.src], t.H, t.W, t.C, t.C, sg.kh, sg.kw, sg.stride, sg.pad,
-                               pk.seg_ksteps[s], kbase};
+                               sg.pad_w >= 0 ? sg.pad_w : sg.pad, pk.seg_ksteps[s], kbase};
         kbase += pk.seg_ksteps[s];
       }
       const int Ho = op.out >= 0 ? plan.tensors[op.out].H : plan.out_h;
@@ -293,7 +297,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const TensorSpec& src = plan.tensors[op.src];
       const TensorSpec& tgt = plan.tensors[op.out];
       p.nseg = 1;
-      p.seg[0] = ConvSegment{base + ws->off[op.src], src.H, src.W, src.C, src.C, 1, 1, 1, 0, pk.seg_ksteps[0], 0};
+      p.seg[0] = ConvSegment{base + ws->off[op.src], src.H, src.W, src.C, src.C, 1, 1, 1, 0, 0, pk.seg_ksteps[0], 0};
       p.Ho = src.H;
       p.Wo = src.W;
       p.M = B * src.H * src.W;
@@ -317,6 +321,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   std::vector<KStep> all_ks;
   std::vector<size_t> ks_off(plan.ops.size(), 0);
   ws->use_pipe.assign(plan.ops.size(), 0);
+  ws->halo_tw.assign(plan.ops.size(), 0);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (op.kind == OP_PREP) continue;
@@ -328,15 +333,19 @@ int Engine::make_workspace(int B, Workspace* ws) {
       for (int kk = 0; kk < sg.ksteps; ++kk) {
         KStep d{};
         d.src = sg.src;
-        d.H = sg.H; d.W = sg.W; d.ldc = sg.ldc; d.stride = sg.stride; d.pad = sg.pad;
-        d.kw = sg.kw; d.ntaps = sg.kh * sg.kw; d.kw_inv = 1.0f / (float)sg.kw;
+        d.seg = s;
+        d.H = sg.H; d.W = sg.W; d.ldc = sg.ldc; d.stride = sg.stride;
+        d.pad_h = sg.pad; d.pad_w = sg.pad_w; d.kh = sg.kh; d.kw = sg.kw;
+        d.kw_inv = 1.0f / (float)sg.kw;
         const int kel = kk * BK;
-        if (sg.C % BK == 0) {
+        const int vec = 16 / esz;
+        if (sg.C % BK == 0 && sg.kh * sg.kw <= 32) {
           const int tap = kel / sg.C;
-          d.mode = 0; d.ky = tap / sg.kw; d.kx = tap % sg.kw; d.c0 = kel % sg.C;
-        } else if (sg.C < BK && (sg.C & (sg.C - 1)) == 0 && d.ntaps + BK / sg.C < 4096) {
-          d.mode = 1; d.tap0 = kel / sg.C;
-          while ((1 << d.cshift) < sg.C) ++d.cshift;
+          d.mode = 0; d.tap = tap;
+          d.off = ((long long)(tap / sg.kw) * sg.W + tap % sg.kw) * sg.ldc + kel % sg.C;
+        } else if (sg.C < BK && sg.C % vec == 0 && (sg.kh * sg.kw + 8) * (sg.C / vec) < (1 << 16)) {
+          d.mode = 1; d.q0 = kel / vec; d.cpt = sg.C / vec;
+          d.cpt_inv = 1.0f / (float)d.cpt;
         } else {
           ok = false;
           break;
@@ -354,6 +363,24 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.mtiles = mt;
     }
     p.zero = zero_page;
+    if (const char* env = std::getenv("TV_ABLATE")) p.ablate = std::atoi(env);
+    // 3x3 / stride 1 / pad 1 single-input convs with whole channel blocks: halo-tile kernel
+    if (halo_mode && op.kind == OP_CONV && op.segs.size() == 1) {
+      const SegSpec& sg = op.segs[0];
+      const ConvSegment& cs = p.seg[0];
+      const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
+      if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand &&
+          cs.C % BK == 0 && cs.ldc % (16 / esz) == 0) {
+        const int t16 = halo_tiles(B, cs.H, cs.W, 16), t32 = halo_tiles(B, cs.H, cs.W, 32);
+        const int tw = t32 <= t16 ? 32 : 16;
+        const int mt = tw == 32 ? t32 : t16;
+        if ((long)mt * p.ntiles >= (halo_mode == 2 ? 1 : 32)) {
+          ws->halo_tw[i] = tw;
+          ws->use_pipe[i] = 0;
+          p.mtiles = mt;
+        }
+      }
+    }
   }
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
@@ -400,8 +427,9 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
-  int rc = ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
-                           : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
+  int rc = ws->halo_tw[i] ? launch_conv_halo(p, ws->dparams + i, p.out, dtype, out_f32, ws->halo_tw[i], s)
+           : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
+                             : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
   if (rc) return rc;
   if (op.kind == OP_CONVT_ADD) {
     const TensorSpec& tgt = plan.tensors[op.out];

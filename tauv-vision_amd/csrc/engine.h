@@ -26,6 +26,7 @@ struct Workspace {
   std::vector<ConvParams> params;   // per op (host copy)
   ConvParams* dparams = nullptr;    // per op (device copy)
   std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
+  std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
 };
 
@@ -38,6 +39,7 @@ struct Engine {
   size_t weight_bytes = 0;
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
   int pipe_mode = -1;          // -1 auto, 0 never, 1 whenever representable (env TV_CONV_PIPE)
+  int halo_mode = 0;           // 1 enables the halo-tile 3x3 kernel, 2 forces it (env TV_CONV_HALO)
   std::mutex mu;
   std::map<std::pair<void*, int>, Workspace*> workspaces;
   std::unordered_map<std::string, std::pair<const float*, int64_t>> host_w;  // during create only

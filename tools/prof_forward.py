@@ -1,0 +1,34 @@
+"""Profiling driver: N forwards of the bench workload (R18, 640x480, fp16) for rocprofv3
+kernel traces / PMC passes. Usage: python tools/prof_forward.py [--batch 64] [--iters 3]"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tauv-vision_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from bench import build_model  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--precision", default="fp16")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    model, oc, sd = build_model(a.precision, dev)
+    frames = torch.randint(0, 256, (a.batch, 480, 640, 3), device=dev, dtype=torch.uint8)
+    eng = model.engine(dev, 480, 640)
+    out = eng.alloc_out(a.batch)
+    for _ in range(a.iters):
+        eng.forward_u8(frames, out)
+    torch.cuda.synchronize()
+    print("done", float(out.float().abs().mean()))
+
+
+if __name__ == "__main__":
+    main()

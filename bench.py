@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 import tauv_vision_amd as tv  # noqa: E402
 from tauv_vision_amd.decode import DeviceDecoder  # noqa: E402
+from tauv_vision_amd.sharding import RecordGather  # noqa: E402
 from tauv_vision_amd.weights import seeded_state_dict  # noqa: E402
 
 HEIGHTS, CHANNELS, DOWNSAMPLES, N_LABELS = [2] * 5, [128] * 6, 2, 4
@@ -55,7 +56,7 @@ class Pipeline:
         self.pred = tv.centernet.prediction_from_nhwc(self.out, oc)
         C, H, W = self.pred.heatmap.shape[1:]
         self.dec = DeviceDecoder(B, C, H, W, K, device)
-        self.mc, self.thr = mc, thr
+        self.mc, self.thr, self.B = mc, thr, B
         self.host = torch.empty((B, K, 10), dtype=torch.float32, pin_memory=True)
         self.host_counts = torch.empty((B,), dtype=torch.int32, pin_memory=True)
 
@@ -70,10 +71,27 @@ class Pipeline:
         self.host_counts.copy_(cnt, non_blocking=True)
 
 
+def load_traffic(kernel, batch, precision):
+    """HBM bytes per launch of `kernel` from the committed PMC profile (tools/traffic.py over
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md),
+    or None when no profile of this exact workload is committed."""
+    path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        t = json.load(f)
+    if t.get("batch") != batch or t.get("precision") != precision:
+        return None
+    k = t.get("kernels", {}).get(kernel)
+    return None if k is None else k["bytes_per_launch"]
+
+
 def conv_roofline(pipe, frames_f32, precision, reps=3):
-    """Per-launch HIP-event timing of the forward (tv_engine_profile, on the launch stream).
-    The dominant kernel is the implicit-GEMM conv (conv_igemm); achieved = its algorithmic
-    FLOPs (2*MAC) / its summed launch durations."""
+    """Per-launch HIP-event timing of one forward (tv_engine_profile: events recorded on the
+    launch stream around every launch; a separate pass after the timed region). The dominant
+    kernel is the conv instance with the largest summed time; achieved = its algorithmic FLOPs
+    (2*MAC per launch) / its summed launch durations (= FLOPs per launch / average
+    launch duration)."""
     best = None
     for _ in range(reps):
         ops = pipe.eng.profile(frames_f32, pipe.out)
@@ -84,17 +102,27 @@ def conv_roofline(pipe, frames_f32, precision, reps=3):
                 b[1] = min(b[1], o[1])
     if os.environ.get("TV_PROFILE_OUT"):
         with open(os.environ["TV_PROFILE_OUT"], "w") as f:
-            json.dump([{"op": o[0], "ms": o[1], "gflop": o[2] / 1e9} for o in best], f, indent=0)
+            json.dump([{"op": o[0], "ms": o[1], "gflop": o[2] / 1e9, "kernel": o[3]} for o in best], f, indent=0)
     conv = [o for o in best if o[2] > 0]
-    ms = sum(o[1] for o in conv)
-    flops = sum(o[2] for o in conv)
+    kern = {}
+    for o in conv:
+        k = kern.setdefault(o[3], [0, 0.0, 0.0])
+        k[0] += 1
+        k[1] += o[1]
+        k[2] += o[2]
+    name, (n, ms, flops) = max(kern.items(), key=lambda kv: kv[1][1])
     achieved = flops / (ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[precision]
-    top = sorted(best, key=lambda o: -o[1])[:8]
+    all_ms = sum(o[1] for o in conv)
+    all_fl = sum(o[2] for o in conv)
+    top = sorted(best, key=lambda o: -o[1])[:6]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None,
-            "kernel": "conv_igemm (all %d conv launches of one forward)" % len(conv),
-            "conv_ms_per_batch": round(ms, 3), "flops_per_batch": flops,
+            "frac": round(achieved / peak, 4),
+            "traffic": load_traffic(name, pipe.B, precision),
+            "kernel": f"{name}: {n} launches/forward, avg {ms / n:.4f} ms, avg {flops / n / 1e9:.2f} GFLOP/launch",
+            "all_conv": {"launches": len(conv), "ms": round(all_ms, 3), "tflops": round(all_fl / all_ms / 1e9, 1)},
+            "per_kernel": {k: {"launches": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / v[1] / 1e9, 1)}
+                           for k, v in kern.items()},
             "top_launches": [{"op": o[0], "ms": round(o[1], 4),
                               "tflops": round(o[2] / max(o[1], 1e-9) / 1e9, 1)} for o in top]}
 
@@ -106,7 +134,8 @@ def cpu_baseline(sd, seconds, K, thr):
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import oracle
     from recipe import normalize
-    torch.set_num_threads(os.cpu_count() or 1)
+    # the host's share of cores: torch's default (OMP_NUM_THREADS; 16 on the GPU box). Setting
+    # os.cpu_count() there oversubscribes the box's CPU share by ~16x.
     g = torch.Generator().manual_seed(1234)
     n, t0 = 0, time.perf_counter()
     with torch.no_grad():
@@ -154,14 +183,8 @@ def main():
     frames = torch.randint(0, 256, (B, H, W, 3), generator=gen, device=device, dtype=torch.uint8)
     pipe = Pipeline(model, oc, mc, B, K, args.thr, device)
 
-    gather = None
-    if world > 1:
-        g_rec = torch.empty((world, B, K, 10), dtype=torch.float32, device=device)
-        g_cnt = torch.empty((world, B), dtype=torch.int32, device=device)
-
-        def gather(rec, cnt):  # detections of every rank on every rank (batched path, RCCL over xGMI)
-            dist.all_gather_into_tensor(g_rec, rec)
-            dist.all_gather_into_tensor(g_cnt, cnt)
+    # detections of every rank on every rank: one RCCL all-gather of the packed records
+    gather = RecordGather(B, K, device) if world > 1 else None
 
     for _ in range(args.warmup):
         pipe.step(frames, gather)

@@ -90,6 +90,9 @@ int tv_engine_forward_u8(tv_engine* engine, const uint8_t* frames_nhwc, int32_t 
 int tv_engine_profile(tv_engine* engine, const float* img_nchw, int32_t batch, float* out_nhwc, void* stream,
                       float* ms, double* flops, int32_t cap, int32_t* n_ops);
 const char* tv_engine_op_label(tv_engine* engine, int32_t index);
+/* Kernel family launch `index` uses at this batch size ("conv_pipe", "conv_igemm", "conv_halo",
+ * "prep"); "" before the batch's workspace exists. Diagnostic (roofline attribution). */
+const char* tv_engine_op_kernel(tv_engine* engine, int32_t batch, int32_t index);
 
 /* heatmap_nms(sigmoid?(heat), k) (decode.py:239-252) over any strided [B,C,H,W] fp32
  * view; `out` is dense [B,C,H,W]. k must be odd and >= 1 (else TV_EINVAL, like the

@@ -136,6 +136,11 @@ const char* tv_engine_op_label(tv_engine* e, int32_t i) {
   return e->e.plan.ops[i].label.c_str();
 }
 
+const char* tv_engine_op_kernel(tv_engine* e, int32_t B, int32_t i) {
+  if (!e || i < 0 || i >= (int)e->e.plan.ops.size()) return "";
+  return e->e.op_kernel(B, i);
+}
+
 int tv_heatmap_nms(const float* heat, const int64_t st[4], int32_t B, int32_t C, int32_t H, int32_t W, int32_t k,
                    int32_t apply_sigmoid, float* out, void* stream) {
   TV_GUARD({

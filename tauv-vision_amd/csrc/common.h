@@ -70,7 +70,11 @@ struct ConvParams {
   const KStep* ks;      // pipelined kernel: one descriptor per k-step (nks of them)
   int nks;
   int ablate;           // timing experiments only (env TV_ABLATE): 1 no main-loop DMA, 2 no MFMA
+  unsigned long long* stamps;  // diagnostics only (env TV_STAMPS): per block kStampWords words
 };
+// per-block stamp record: s_memtime at entry, first stage landed, main loop done, end;
+// s_memrealtime at entry and end; HW_ID; XCC_ID
+constexpr int kStampWords = 8;
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
 int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
@@ -82,6 +86,14 @@ constexpr int kPipeTileM = 256;
 int launch_conv_halo(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int tw,
                      hipStream_t s);
 int halo_tiles(int B, int H, int W, int tw);
+
+// Persistent halo-tile 3x3 / stride 1 / pad 1 kernel (conv3x3.hip), fp16/bf16: 512-pixel
+// tiles of tw (16 or 32) columns; ConvParams.mtiles = conv3x3_tiles(B, H, W, tw); `grid`
+// persistent workgroups (one per CU, a multiple of 8 when >= 8).
+constexpr int kConv3MaxN = 1024;
+int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
+                   hipStream_t s);
+int conv3x3_tiles(int B, int H, int W, int tw);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,

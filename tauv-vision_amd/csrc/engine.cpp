@@ -196,6 +196,12 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   TV_HIP(hipMalloc(&zero_page, 256));
   TV_HIP(hipMemset(zero_page, 0, 256));
   if (const char* env = std::getenv("TV_CONV_PIPE")) pipe_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_CONV3")) conv3_mode = std::atoi(env);
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+      cu_count = ncu;
+  }
   if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
   packed.resize(plan.ops.size());
   for (size_t i = 0; i < plan.ops.size(); ++i) {
@@ -321,7 +327,10 @@ int Engine::make_workspace(int B, Workspace* ws) {
   std::vector<KStep> all_ks;
   std::vector<size_t> ks_off(plan.ops.size(), 0);
   ws->use_pipe.assign(plan.ops.size(), 0);
+  ws->kname.assign(plan.ops.size(), std::string());
   ws->halo_tw.assign(plan.ops.size(), 0);
+  ws->c3_tw.assign(plan.ops.size(), 0);
+  ws->c3_grid.assign(plan.ops.size(), 0);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (op.kind == OP_PREP) continue;
@@ -381,12 +390,44 @@ int Engine::make_workspace(int B, Workspace* ws) {
         }
       }
     }
+    // persistent halo-tile 3x3 kernel (conv3x3.hip): 3x3 / stride 1 / pad 1, one input of 128
+    // channels, fp16/bf16, 16-byte aligned channel slices, byte offsets within 2^31
+    if (conv3_mode && dtype != F32 && op.kind == OP_CONV && op.segs.size() == 1 && op.out >= 0) {
+      const SegSpec& sg = op.segs[0];
+      const ConvSegment& cs = p.seg[0];
+      const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
+      const size_t src_bytes = (size_t)B * cs.H * cs.W * cs.ldc * esz;
+      if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand && cs.C == 128 &&
+          cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && src_bytes < (1ull << 31) &&
+          p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2) {
+        const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16), t32 = conv3x3_tiles(B, cs.H, cs.W, 32);
+        const int tw = t32 <= t16 ? 32 : 16;
+        const int mt = tw == 32 ? t32 : t16;
+        long total = (long)mt * p.ntiles;
+        int grid = (int)std::min<long>(total, cu_count);
+        if (grid >= 8) grid -= grid % 8;
+        ws->c3_tw[i] = tw;
+        ws->c3_grid[i] = grid;
+        ws->halo_tw[i] = 0;
+        ws->use_pipe[i] = 0;
+        p.mtiles = mt;
+      }
+    }
   }
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
     for (size_t i = 0; i < plan.ops.size(); ++i)
       if (ws->use_pipe[i]) ws->params[i].ks = ws->dks + ks_off[i];
+  }
+  if (std::getenv("TV_STAMPS")) {  // diagnostics: per-block phase timestamps of pipelined convs
+    ws->stamps.assign(plan.ops.size(), nullptr);
+    for (size_t i = 0; i < plan.ops.size(); ++i) {
+      if (!ws->use_pipe[i]) continue;
+      ConvParams& p = ws->params[i];
+      TV_HIP(hipMalloc((void**)&ws->stamps[i], (size_t)p.mtiles * p.ntiles * kStampWords * 8));
+      p.stamps = ws->stamps[i];
+    }
   }
   TV_HIP(hipMalloc((void**)&ws->dparams, ws->params.size() * sizeof(ConvParams)));
   TV_HIP(hipMemcpy(ws->dparams, ws->params.data(), ws->params.size() * sizeof(ConvParams), hipMemcpyHostToDevice));
@@ -427,7 +468,8 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
-  int rc = ws->halo_tw[i] ? launch_conv_halo(p, ws->dparams + i, p.out, dtype, out_f32, ws->halo_tw[i], s)
+  int rc = ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s)
+           : ws->halo_tw[i] ? launch_conv_halo(p, ws->dparams + i, p.out, dtype, out_f32, ws->halo_tw[i], s)
            : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
                              : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
   if (rc) return rc;
@@ -460,6 +502,30 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
   return TV_OK;
 }
 
+const char* Engine::op_kernel(int B, size_t i) {
+  std::lock_guard<std::mutex> g(mu);
+  for (const auto& kv : workspaces) {
+    if (kv.first.second != B) continue;
+    Workspace* ws = kv.second;
+    // the kernel instance as rocprofv3 demangles it (template <T, OutT, MODE or TW>)
+    static const char* tn[3] = {"float", "_Float16", "__bf16"};
+    const OpSpec& op = plan.ops[i];
+    if (op.kind == OP_PREP) return "prep";
+    const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
+    const char* t = tn[dtype];
+    const char* o = (op.out < 0) ? "float" : t;
+    std::string& name = ws->kname[i];
+    if (name.empty()) {
+      if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + o + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ">";
+      else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";
+      else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
+      else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";
+    }
+    return name.c_str();
+  }
+  return "";
+}
+
 int Engine::profile(const float* img, int B, float* out, hipStream_t s, float* ms, double* flops, int cap,
                     int* n_ops) {
   TV_HIP(hipSetDevice(device));
@@ -484,6 +550,19 @@ int Engine::profile(const float* img, int B, float* out, hipStream_t s, float* m
       flops[i] = plan.ops[i].flops * B;
     }
     *n_ops = (int)n;
+    if (const char* path = std::getenv("TV_STAMPS")) {
+      for (size_t i = 0; i < n && i < ws->stamps.size(); ++i) {
+        if (!ws->stamps[i]) continue;
+        const ConvParams& p = ws->params[i];
+        std::vector<unsigned long long> h((size_t)p.mtiles * p.ntiles * kStampWords);
+        TV_HIP(hipMemcpy(h.data(), ws->stamps[i], h.size() * 8, hipMemcpyDeviceToHost));
+        const std::string f = std::string(path) + "_" + std::to_string(i) + ".bin";
+        if (FILE* fp = std::fopen(f.c_str(), "wb")) {
+          std::fwrite(h.data(), 8, h.size(), fp);
+          std::fclose(fp);
+        }
+      }
+    }
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;

@@ -27,7 +27,10 @@ struct Workspace {
   ConvParams* dparams = nullptr;    // per op (device copy)
   std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
   std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
+  std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
+  std::vector<unsigned long long*> stamps;  // diagnostics (env TV_STAMPS), per op
+  std::vector<std::string> kname;   // per op: kernel instance name (diagnostics), filled lazily
 };
 
 struct Engine {
@@ -39,6 +42,8 @@ struct Engine {
   size_t weight_bytes = 0;
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
   int pipe_mode = -1;          // -1 auto, 0 never, 1 whenever representable (env TV_CONV_PIPE)
+  int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
+  int cu_count = 256;          // compute units (persistent grids)
   int halo_mode = 0;           // 1 enables the halo-tile 3x3 kernel, 2 forces it (env TV_CONV_HALO)
   std::mutex mu;
   std::map<std::pair<void*, int>, Workspace*> workspaces;
@@ -49,6 +54,7 @@ struct Engine {
   int get_workspace(int B, hipStream_t s, Workspace** out);
   int forward(const void* input, int input_u8, int B, float* out, hipStream_t s);
   int profile(const float* img, int B, float* out, hipStream_t s, float* ms, double* flops, int cap, int* n_ops);
+  const char* op_kernel(int B, size_t i);
 
  private:
   const float* weight(const std::string& name, int64_t numel);

@@ -152,17 +152,8 @@ def decode(prediction, model_config, n_detections: int, score_threshold: float) 
     records, counts = _records(prediction.heatmap, prediction.size, prediction.offset, prediction.depth,
                                n_detections, 0, model_config.downsample_ratio, model_config.in_h, model_config.in_w,
                                score_threshold)
-    out = []
-    for b in range(records.shape[0]):
-        dets = []
-        for r in records[b, :counts[b]]:
-            d = Detection(label=torch.tensor(int(r[0])), score=torch.tensor(r[1]), y=float(r[2]), x=float(r[3]),
-                          h=float(r[4]), w=float(r[5]))
-            if has_depth:
-                d.depth = float(r[6])
-            dets.append(d)
-        out.append(dets)
-    return out
+    from .sharding import records_to_detections
+    return records_to_detections(records, counts, has_depth)
 
 
 def decode_keypoints(prediction, model_config, object_config, M_projection, n_detections: int,

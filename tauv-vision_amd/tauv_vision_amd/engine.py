@@ -70,7 +70,7 @@ class NativeEngine:
         return out
 
     def profile(self, img, out=None, cap=4096):
-        """Per-launch (label, ms, flops) of one forward, timed with HIP events."""
+        """Per-launch (label, ms, flops, kernel) of one forward, timed with HIP events."""
         B = img.shape[0]
         if out is None:
             out = self.alloc_out(B)
@@ -80,4 +80,5 @@ class NativeEngine:
         L = _lib.lib()
         _lib.check(L.tv_engine_profile(self._h, ctypes.c_void_p(img.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
                                        _lib.stream_of(self.device), ms, fl, cap, ctypes.byref(n)), "profile")
-        return [(L.tv_engine_op_label(self._h, i).decode(), ms[i], fl[i]) for i in range(min(n.value, cap))]
+        return [(L.tv_engine_op_label(self._h, i).decode(), ms[i], fl[i], L.tv_engine_op_kernel(self._h, B, i).decode())
+                for i in range(min(n.value, cap))]

@@ -1,0 +1,64 @@
+"""HBM traffic per kernel instance from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; one
+pass each, tools/prof_forward.py --iters 1 = one forward of the bench workload).
+
+FETCH_SIZE / WRITE_SIZE are KiB. On gfx950 FETCH_SIZE counts exactly half the bytes of 16-B/lane
+streaming reads (MI355X_MICROARCH.md, HBM section), so it is doubled; WRITE_SIZE is exact for
+16-B/lane stores. Usage:
+  python tools/traffic.py <FETCH_SIZE_counter_collection.csv> <WRITE_SIZE_counter_collection.csv> \
+      --batch 64 --precision fp16 -o profiles/hbm_traffic.json
+"""
+import argparse
+import collections
+import csv
+import json
+import subprocess
+
+
+def demangle(name):
+    if not name.startswith("_Z"):
+        return name
+    out = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
+    out = out[5:] if out.startswith("void ") else out
+    return out.split("(")[0]
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(lambda: [0, 0.0])
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            k = acc[demangle(r["Kernel_Name"])]
+            k[0] += 1
+            k[1] += float(r["Counter_Value"]) * 1024.0
+    return acc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--precision", default="fp16")
+    ap.add_argument("-o", "--out", default="profiles/hbm_traffic.json")
+    a = ap.parse_args()
+    fe, wr = per_kernel(a.fetch, "FETCH_SIZE"), per_kernel(a.write, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fe) | set(wr)):
+        n = max(fe[k][0], wr[k][0])
+        fb, wb = 2.0 * fe[k][1], wr[k][1]
+        kernels[k] = {"launches": n, "fetch_bytes": fb, "write_bytes": wb,
+                      "bytes_per_launch": (fb + wb) / max(n, 1)}
+    res = {"batch": a.batch, "precision": a.precision,
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, one forward (tools/prof_forward.py --iters 1); "
+                     "FETCH_SIZE x2 (gfx950), KiB -> bytes",
+           "total_bytes": sum(v["fetch_bytes"] + v["write_bytes"] for v in kernels.values()),
+           "kernels": kernels}
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+    for k, v in sorted(kernels.items(), key=lambda kv: -(kv[1]["fetch_bytes"] + kv[1]["write_bytes"])):
+        print(f"{v['launches']:4d} {v['fetch_bytes'] / 1e9:8.3f} GB rd {v['write_bytes'] / 1e9:8.3f} GB wr  {k}")
+
+
+if __name__ == "__main__":
+    main()

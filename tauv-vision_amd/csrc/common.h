@@ -74,7 +74,8 @@ struct ConvParams {
 };
 // per-block stamp record: s_memtime at entry, first stage landed, main loop done, end;
 // s_memrealtime at entry and end; HW_ID; XCC_ID
-constexpr int kStampWords = 8;
+// (+ persistent kernels: [8] cycles stalled in waits/barriers, [9] epilogue cycles, [10] tiles)
+constexpr int kStampWords = 12;
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
 int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
@@ -94,6 +95,9 @@ constexpr int kConv3MaxN = 1024;
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
                    hipStream_t s);
 int conv3x3_tiles(int B, int H, int W, int tw);
+// k-step-major, pre-swizzled weight copy the kernel streams (from the [Npad][Kpad] packing)
+size_t conv3x3_weight_bytes(int ntiles);
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, void* out, hipStream_t s);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,

@@ -216,6 +216,7 @@ Engine::~Engine() {
   if (zero_page) (void)hipFree(zero_page);
   for (auto& p : packed) {
     if (p.w) (void)hipFree(p.w);
+    if (p.w_c3) (void)hipFree(p.w_c3);
     if (p.bias) (void)hipFree(p.bias);
   }
   for (auto& kv : workspaces) {
@@ -406,6 +407,14 @@ int Engine::make_workspace(int B, Workspace* ws) {
         long total = (long)mt * p.ntiles;
         int grid = (int)std::min<long>(total, cu_count);
         if (grid >= 8) grid -= grid % 8;
+        Packed& pk3 = packed[i];
+        if (!pk3.w_c3) {
+          TV_HIP(hipMalloc(&pk3.w_c3, conv3x3_weight_bytes(p.ntiles)));
+          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, pk3.w_c3, nullptr);
+          if (rc) return rc;
+          TV_HIP(hipDeviceSynchronize());
+        }
+        p.weight = pk3.w_c3;
         ws->c3_tw[i] = tw;
         ws->c3_grid[i] = grid;
         ws->halo_tw[i] = 0;
@@ -423,9 +432,11 @@ int Engine::make_workspace(int B, Workspace* ws) {
   if (std::getenv("TV_STAMPS")) {  // diagnostics: per-block phase timestamps of pipelined convs
     ws->stamps.assign(plan.ops.size(), nullptr);
     for (size_t i = 0; i < plan.ops.size(); ++i) {
-      if (!ws->use_pipe[i]) continue;
+      if (!ws->use_pipe[i] && !ws->c3_tw[i]) continue;
       ConvParams& p = ws->params[i];
-      TV_HIP(hipMalloc((void**)&ws->stamps[i], (size_t)p.mtiles * p.ntiles * kStampWords * 8));
+      const size_t nb = ws->c3_tw[i] ? (size_t)ws->c3_grid[i] : (size_t)p.mtiles * p.ntiles;
+      TV_HIP(hipMalloc((void**)&ws->stamps[i], nb * kStampWords * 8));
+      TV_HIP(hipMemset(ws->stamps[i], 0, nb * kStampWords * 8));
       p.stamps = ws->stamps[i];
     }
   }
@@ -554,7 +565,8 @@ int Engine::profile(const float* img, int B, float* out, hipStream_t s, float* m
       for (size_t i = 0; i < n && i < ws->stamps.size(); ++i) {
         if (!ws->stamps[i]) continue;
         const ConvParams& p = ws->params[i];
-        std::vector<unsigned long long> h((size_t)p.mtiles * p.ntiles * kStampWords);
+        const size_t nb = ws->c3_tw[i] ? (size_t)ws->c3_grid[i] : (size_t)p.mtiles * p.ntiles;
+        std::vector<unsigned long long> h(nb * kStampWords);
         TV_HIP(hipMemcpy(h.data(), ws->stamps[i], h.size() * 8, hipMemcpyDeviceToHost));
         const std::string f = std::string(path) + "_" + std::to_string(i) + ".bin";
         if (FILE* fp = std::fopen(f.c_str(), "wb")) {

@@ -13,6 +13,7 @@ namespace tv {
 
 struct Packed {
   void* w = nullptr;       // [Npad][Kpad] compute dtype
+  void* w_c3 = nullptr;    // conv3x3.hip k-step-major copy (made on first use)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;

@@ -8,7 +8,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtauv_vision_amd.so")
+# TV_LIB: load an alternative build of the library (kernel A/B experiments)
+LIB_PATH = os.environ.get("TV_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libtauv_vision_amd.so")
 
 TV_OK, TV_EINVAL, TV_ESHAPE, TV_EHIP, TV_ENOTFOUND, TV_ENOMEM = range(6)
 DTYPES = {"fp32": 0, "fp16": 1, "bf16": 2}

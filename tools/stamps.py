@@ -15,7 +15,21 @@ def main():
         labels = {i: o["op"] for i, o in enumerate(json.load(open(sys.argv[2])))}
     for f in sorted(glob.glob(pre + "_*.bin"), key=lambda x: int(x.rsplit("_", 1)[1][:-4])):
         i = int(f.rsplit("_", 1)[1][:-4])
-        a = np.fromfile(f, dtype=np.uint64).reshape(-1, 8).astype(np.int64)
+        a = np.fromfile(f, dtype=np.uint64).reshape(-1, 12).astype(np.int64)
+        if a[:, 10].max() > 0:  # persistent kernel: per-block totals
+            a = a[a[:, 0] > 0]
+            st, rt = a[:, :4], a[:, 4:6]
+            ghz = np.median((st[:, 3] - st[:, 0]) / np.maximum(rt[:, 1] - rt[:, 0], 1) * 0.1)
+            tiles = a[:, 10]
+            tot = st[:, 3] - st[:, 0]
+            span_us = (rt[:, 1].max() - rt[:, 0].min()) / 100.0
+            print(f"op {i:3d} persistent blocks {len(a):4d} tiles/blk {np.median(tiles):5.1f} clk {ghz:.2f}GHz "
+                  f"per tile cyc: total {np.median(tot / tiles):7.0f} stall {np.median(a[:, 8] / tiles):7.0f} "
+                  f"epi {np.median(a[:, 9] / tiles):6.0f} | prologue {np.median(st[:, 1] - st[:, 0]):6.0f} "
+                  f"steps/tile {np.median(a[:, 11] / tiles):4.0f} span {span_us:7.1f}us "
+                  f"start spread {(rt[:, 0].max() - rt[:, 0].min()) / 100.0:5.1f}us "
+                  f"end spread {(rt[:, 1].max() - rt[:, 1].min()) / 100.0:5.1f}us  {labels.get(i, '')}")
+            continue
         st = a[:, :4]
         rt = a[:, 4:6]
         ghz = np.median((st[:, 3] - st[:, 0]) / np.maximum(rt[:, 1] - rt[:, 0], 1) * 0.1)

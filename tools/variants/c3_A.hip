@@ -377,14 +377,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
-    if (s + D < S_tot) w_piece();
-    mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
     read_one(IC<2>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<3>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+    read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+    read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
+    if (s + D < S_tot) w_piece();
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
     if constexpr (TAP == 0) {
       if (nxt_exists && nxt_newtile) {
         int fr, y0, x0, nt;
@@ -394,8 +397,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<2>{}, IC<FIRST>{}, H0);
-    read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     if constexpr (TAP < HTAPS)
       if (nxt_exists) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);
     __builtin_amdgcn_sched_barrier(0);
@@ -403,24 +404,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
     __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<0>{}, IC<false>{}, H1);
+    // second half: sub-step 1 MFMAs; the next k-step's sub-step 0 reads go out first (H0 free)
     if (do_r) {
       read_one(IC<0>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<1>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<1>{}, IC<false>{}, H1);
-    if (do_r) {
       read_one(IC<2>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<3>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<2>{}, IC<false>{}, H1);
-    if (do_r) {
       read_one(IC<4>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<5>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
     }
     __builtin_amdgcn_sched_barrier(0);
+    mfma_pair(IC<0>{}, IC<false>{}, H1);
+    mfma_pair(IC<1>{}, IC<false>{}, H1);
+    mfma_pair(IC<2>{}, IC<false>{}, H1);
     mfma_pair(IC<3>{}, IC<false>{}, H1);
     __builtin_amdgcn_sched_barrier(0);
     ++s;

@@ -377,10 +377,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
-    if (s + D < S_tot) w_piece();
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+    if (s + D < S_tot) w_piece();
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
     read_one(IC<2>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);

@@ -255,9 +255,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   for (int j = 0; j < 2; ++j)
     wa[j] = lds0 + OFF_W + (unsigned)(l32 * 64 + (((2 * j + lh) ^ ((l32 >> 2) & 3)) << 4));
 
+  bool abl_done = false;
   // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]
   auto read_one = [&](auto r, auto j, auto tap, unsigned xb, unsigned wb, Half& F) __attribute__((always_inline)) {
     constexpr int R = decltype(r)::value, J = decltype(j)::value, TAP = decltype(tap)::value;
+#ifdef ABL_NOREAD
+    if (abl_done) return;
+#endif
     constexpr int TOFF = ((TAP / 3) * RS + (TAP % 3)) * PITCH;
     if constexpr (R < 2) F.x[R] = ds_read16<TOFF + 32 * J + R * FOFF>(xb);
     else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
@@ -336,6 +340,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   if (p.stamps) st1 = __builtin_amdgcn_s_memtime();
+  abl_done = true;
 
   int s = 0;   // global k-step
   int tl = 0;  // tile index within this block's list
@@ -364,7 +369,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     if (p.stamps) tw0 = __builtin_amdgcn_s_memtime();
     wait_vm_n(s + 1 < S_tot ? younger : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifndef ABL_NOBAR
     __builtin_amdgcn_s_barrier();
+#endif
     __builtin_amdgcn_sched_barrier(0);
     if (p.stamps) stall += __builtin_amdgcn_s_memtime() - tw0;
 
@@ -377,7 +384,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
+#ifndef ABL_NODMA
     if (s + D < S_tot) w_piece();
+#endif
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
@@ -396,8 +405,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     mfma_pair(IC<2>{}, IC<FIRST>{}, H0);
     read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+#ifndef ABL_NODMA
     if constexpr (TAP < HTAPS)
       if (nxt_exists) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<3>{}, IC<FIRST>{}, H0);
     __builtin_amdgcn_sched_barrier(0);

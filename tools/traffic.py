@@ -17,7 +17,9 @@ import subprocess
 def demangle(name):
     if not name.startswith("_Z"):
         return name
-    out = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip()
+    # binutils' c++filt predates the _Float16 mangling (DF16_): demangle it as 'half' and rename
+    out = subprocess.run(["c++filt", name.replace("DF16_", "Dh")], capture_output=True, text=True).stdout.strip()
+    out = out.replace("half", "_Float16")
     out = out[5:] if out.startswith("void ") else out
     return out.split("(")[0]
 

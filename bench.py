@@ -86,7 +86,7 @@ def load_traffic(kernel, batch, precision):
     return None if k is None else k["bytes_per_launch"]
 
 
-def conv_roofline(pipe, frames_f32, precision, reps=3):
+def conv_roofline(pipe, frames, precision, reps=3):
     """Per-launch HIP-event timing of one forward (tv_engine_profile: events recorded on the
     launch stream around every launch; a separate pass after the timed region). The dominant
     kernel is the conv instance with the largest summed time; achieved = its algorithmic FLOPs
@@ -94,7 +94,7 @@ def conv_roofline(pipe, frames_f32, precision, reps=3):
     launch duration)."""
     best = None
     for _ in range(reps):
-        ops = pipe.eng.profile(frames_f32, pipe.out)
+        ops = pipe.eng.profile(frames, pipe.out)
         if best is None:
             best = [list(o) for o in ops]
         else:
@@ -207,11 +207,7 @@ def main():
     value = world * B * args.steps / elapsed
 
     # roofline of the dominant kernel (separate pass with per-launch events)
-    frames_f32 = ((frames.permute(0, 3, 1, 2).float() / 255.0 -
-                   torch.tensor([0.485, 0.456, 0.406], device=device).view(1, 3, 1, 1)) /
-                  torch.tensor([0.229, 0.224, 0.225], device=device).view(1, 3, 1, 1)).contiguous()
-    roof = conv_roofline(pipe, frames_f32, args.precision)
-    del frames_f32
+    roof = conv_roofline(pipe, frames, args.precision)
     flops_frame = pipe.eng.geom["flops_per_frame"]
 
     b1 = None

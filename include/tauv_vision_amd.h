@@ -89,6 +89,9 @@ int tv_engine_forward_u8(tv_engine* engine, const uint8_t* frames_nhwc, int32_t 
  * per launch i < *n_ops (cap entries max); label(i) describes launch i. */
 int tv_engine_profile(tv_engine* engine, const float* img_nchw, int32_t batch, float* out_nhwc, void* stream,
                       float* ms, double* flops, int32_t cap, int32_t* n_ops);
+/* The same over raw u8 frames (the tv_engine_forward_u8 path). */
+int tv_engine_profile_u8(tv_engine* engine, const uint8_t* frames_nhwc, int32_t batch, float* out_nhwc,
+                         void* stream, float* ms, double* flops, int32_t cap, int32_t* n_ops);
 const char* tv_engine_op_label(tv_engine* engine, int32_t index);
 /* Kernel family launch `index` uses at this batch size ("conv_pipe", "conv_igemm", "conv_halo",
  * "prep"); "" before the batch's workspace exists. Diagnostic (roofline attribution). */

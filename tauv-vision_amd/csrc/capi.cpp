@@ -125,7 +125,18 @@ int tv_engine_profile(tv_engine* e, const float* img, int32_t B, float* out, voi
   TV_GUARD({
     if (!e || !ms || !flops || !n_ops) { set_error("null argument"); return TV_EINVAL; }
     int n = 0;
-    int rc = e->e.profile(img, B, out, (hipStream_t)stream, ms, flops, cap, &n);
+    int rc = e->e.profile(img, 0, B, out, (hipStream_t)stream, ms, flops, cap, &n);
+    *n_ops = n;
+    return rc;
+  })
+}
+
+int tv_engine_profile_u8(tv_engine* e, const uint8_t* frames, int32_t B, float* out, void* stream, float* ms,
+                         double* flops, int32_t cap, int32_t* n_ops) {
+  TV_GUARD({
+    if (!e || !ms || !flops || !n_ops) { set_error("null argument"); return TV_EINVAL; }
+    int n = 0;
+    int rc = e->e.profile(frames, 1, B, out, (hipStream_t)stream, ms, flops, cap, &n);
     *n_ops = n;
     return rc;
   })

@@ -103,6 +103,21 @@ int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, void* out, hipS
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
                 hipStream_t s);
 
+// Fused input staging + 7x7 stem conv (stem.hip), fp16/bf16, C0 <= 128 output channels.
+struct StemParams {
+  const void* input;  // u8 NHWC [B,H,W,3] frames (u8 = 1) or normalised fp32 NCHW [B,3,H,W]
+  int u8;
+  int B, H, W;
+  void* out;          // NHWC compute dtype, pixel stride out_ldc
+  int out_ldc, N;
+  const void* weight; // stem_weight_bytes() in B-fragment order (stem_fragment_order)
+  const float* bias;  // [>= N] fp32, BN folded
+  int ablate;         // timing experiments only (env TV_STEM_ABLATE): 1 no stores, 2 no MFMA, 4 no staging
+};
+size_t stem_weight_bytes();
+void stem_fragment_order(const uint16_t* w, int Npad, int Kpad, uint16_t* out);
+int launch_stem(const StemParams& p, int dtype, int grid, hipStream_t s);
+
 // ---- small kernels -----------------------------------------------------------------
 int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad, int dtype,
                      hipStream_t s);

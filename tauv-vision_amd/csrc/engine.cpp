@@ -171,6 +171,12 @@ int Engine::pack_op(size_t oi) {
   // device copies
   std::vector<uint8_t> hbuf((size_t)pk.Npad * pk.Kpad * esz);
   for (size_t i = 0; i < hw.size(); ++i) store_elem(hbuf.data(), i, hw[i], dtype);
+  if ((int)oi == stem_op) {  // stem.hip streams its weights in MFMA B-fragment order
+    std::vector<uint8_t> frag(stem_weight_bytes());
+    stem_fragment_order(reinterpret_cast<const uint16_t*>(hbuf.data()), pk.Npad, pk.Kpad,
+                        reinterpret_cast<uint16_t*>(frag.data()));
+    hbuf.swap(frag);
+  }
   TV_HIP(hipMalloc(&pk.w, hbuf.size()));
   TV_HIP(hipMemcpy(pk.w, hbuf.data(), hbuf.size(), hipMemcpyHostToDevice));
   TV_HIP(hipMalloc((void**)&pk.bias, bias.size() * sizeof(float)));
@@ -203,6 +209,16 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
       cu_count = ncu;
   }
   if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
+  // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
+  if (stem_mode && dtype != F32)
+    for (size_t i = 0; i + 1 < plan.ops.size(); ++i)
+      if (plan.ops[i].kind == OP_PREP && plan.ops[i + 1].kind == OP_CONV && plan.ops[i + 1].segs.size() == 1 &&
+          plan.ops[i + 1].segs[0].row_expand == 7 && plan.ops[i + 1].N <= 128 && plan.ops[i + 1].N % 8 == 0 &&
+          plan.ops[i + 1].act == 1) {
+        stem_op = (int)i + 1;
+        break;
+      }
   packed.resize(plan.ops.size());
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     rc = pack_op(i);
@@ -249,7 +265,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     live.erase(std::remove_if(live.begin(), live.end(), [&](const Live& l) { return l.last < (int)i; }), live.end());
-    if (op.out < 0) continue;
+    if (op.out < 0 || (stem_op >= 0 && op.kind == OP_PREP)) continue;  // fused stem: no staged input
     const TensorSpec& t = plan.tensors[op.out];
     size_t sz = align_up((size_t)B * t.H * t.W * t.C * esz, 256);
     std::sort(live.begin(), live.end(), [](const Live& a, const Live& b) { return a.off < b.off; });
@@ -470,6 +486,22 @@ int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
 int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, float* out, hipStream_t s) {
   const OpSpec& op = plan.ops[i];
   char* base = (char*)ws->arena;
+  if (stem_op >= 0 && op.kind == OP_PREP) return TV_OK;  // staging runs inside the stem kernel
+  if ((int)i == stem_op) {
+    StemParams sp{};
+    sp.input = input;
+    sp.u8 = input_u8;
+    sp.B = ws->B;
+    sp.H = desc.in_h;
+    sp.W = desc.in_w;
+    sp.out = base + ws->off[op.out];
+    sp.out_ldc = plan.tensors[op.out].C;
+    sp.N = op.N;
+    sp.weight = packed[i].w;
+    sp.bias = packed[i].bias;
+    if (const char* env = std::getenv("TV_STEM_ABLATE")) sp.ablate = std::atoi(env);
+    return launch_stem(sp, dtype, cu_count, s);
+  }
   if (op.kind == OP_PREP) {
     void* dst = base + ws->off[op.out];
     return input_u8 ? launch_prep_u8((const uint8_t*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s)
@@ -521,7 +553,12 @@ const char* Engine::op_kernel(int B, size_t i) {
     // the kernel instance as rocprofv3 demangles it (template <T, OutT, MODE or TW>)
     static const char* tn[3] = {"float", "_Float16", "__bf16"};
     const OpSpec& op = plan.ops[i];
-    if (op.kind == OP_PREP) return "prep";
+    if (op.kind == OP_PREP) return stem_op >= 0 ? "prep (fused into the stem)" : "prep";
+    if ((int)i == stem_op) {
+      static const char* sn[2][2] = {{"tv::stem::stem_conv<_Float16, false>", "tv::stem::stem_conv<_Float16, true>"},
+                                     {"tv::stem::stem_conv<__bf16, false>", "tv::stem::stem_conv<__bf16, true>"}};
+      return sn[dtype == BF16][profiled_u8 ? 1 : 0];
+    }
     const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
     const char* t = tn[dtype];
     const char* o = (op.out < 0) ? "float" : t;
@@ -537,8 +574,9 @@ const char* Engine::op_kernel(int B, size_t i) {
   return "";
 }
 
-int Engine::profile(const float* img, int B, float* out, hipStream_t s, float* ms, double* flops, int cap,
-                    int* n_ops) {
+int Engine::profile(const void* input, int input_u8, int B, float* out, hipStream_t s, float* ms, double* flops,
+                    int cap, int* n_ops) {
+  profiled_u8 = input_u8;
   TV_HIP(hipSetDevice(device));
   Workspace* ws = nullptr;
   int rc = get_workspace(B, s, &ws);
@@ -548,7 +586,7 @@ int Engine::profile(const float* img, int B, float* out, hipStream_t s, float* m
   for (auto& e : ev) TV_HIP(hipEventCreate(&e));
   TV_HIP(hipEventRecord(ev[0], s));
   for (size_t i = 0; i < n; ++i) {
-    rc = run_op(i, ws, img, 0, out, s);
+    rc = run_op(i, ws, input, input_u8, out, s);
     if (rc) break;
     TV_HIP(hipEventRecord(ev[i + 1], s));
   }

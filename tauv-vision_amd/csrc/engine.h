@@ -45,6 +45,9 @@ struct Engine {
   int pipe_mode = -1;          // -1 auto, 0 never, 1 whenever representable (env TV_CONV_PIPE)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
   int cu_count = 256;          // compute units (persistent grids)
+  int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
+  int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
+  int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1
   int halo_mode = 0;           // 1 enables the halo-tile 3x3 kernel, 2 forces it (env TV_CONV_HALO)
   std::mutex mu;
   std::map<std::pair<void*, int>, Workspace*> workspaces;
@@ -54,7 +57,7 @@ struct Engine {
   int create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev);
   int get_workspace(int B, hipStream_t s, Workspace** out);
   int forward(const void* input, int input_u8, int B, float* out, hipStream_t s);
-  int profile(const float* img, int B, float* out, hipStream_t s, float* ms, double* flops, int cap, int* n_ops);
+  int profile(const void* input, int input_u8, int B, float* out, hipStream_t s, float* ms, double* flops, int cap, int* n_ops);
   const char* op_kernel(int B, size_t i);
 
  private:

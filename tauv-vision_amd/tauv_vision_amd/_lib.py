@@ -41,6 +41,8 @@ EXPORTS = {
     "tv_engine_forward_u8": ([c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
     "tv_engine_profile": ([c_vp, c_vp, c_i32, c_vp, c_vp, ctypes.POINTER(c_f32), ctypes.POINTER(c_f64), c_i32,
                            ctypes.POINTER(c_i32)], c_i32),
+    "tv_engine_profile_u8": ([c_vp, c_vp, c_i32, c_vp, c_vp, ctypes.POINTER(c_f32), ctypes.POINTER(c_f64), c_i32,
+                              ctypes.POINTER(c_i32)], c_i32),
     "tv_engine_op_label": ([c_vp, c_i32], ctypes.c_char_p),
     "tv_engine_op_kernel": ([c_vp, c_i32, c_i32], ctypes.c_char_p),
     "tv_heatmap_nms": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp], c_i32),

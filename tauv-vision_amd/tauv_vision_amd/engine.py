@@ -70,7 +70,8 @@ class NativeEngine:
         return out
 
     def profile(self, img, out=None, cap=4096):
-        """Per-launch (label, ms, flops, kernel) of one forward, timed with HIP events."""
+        """Per-launch (label, ms, flops, kernel) of one forward, timed with HIP events. `img` is the
+        normalised fp32 NCHW input of forward() or uint8 NHWC frames (the forward_u8 path)."""
         B = img.shape[0]
         if out is None:
             out = self.alloc_out(B)
@@ -78,7 +79,8 @@ class NativeEngine:
         fl = (ctypes.c_double * cap)()
         n = ctypes.c_int32()
         L = _lib.lib()
-        _lib.check(L.tv_engine_profile(self._h, ctypes.c_void_p(img.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
+        fn = L.tv_engine_profile_u8 if img.dtype == torch.uint8 else L.tv_engine_profile
+        _lib.check(fn(self._h, ctypes.c_void_p(img.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
                                        _lib.stream_of(self.device), ms, fl, cap, ctypes.byref(n)), "profile")
         return [(L.tv_engine_op_label(self._h, i).decode(), ms[i], fl[i], L.tv_engine_op_kernel(self._h, B, i).decode())
                 for i in range(min(n.value, cap))]

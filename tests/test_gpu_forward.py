@@ -84,7 +84,8 @@ def test_forward_fp32_full_size_r18():
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-@pytest.mark.parametrize("name", ["r18_c16_b2_96x128", "square_c32_b2_128", "r18_c128_b1_480x640"])
+@pytest.mark.parametrize("name", ["r18_c16_b2_96x128", "square_c32_b2_128", "r18_c128_b1_480x640",
+                                  "torpedo_c16_b1_360x640"])
 def test_forward_low_precision(name, precision):
     model, oc, mc, case = build(name, precision)
     pred = model(case_input(name).cuda())
@@ -118,11 +119,17 @@ def test_decode_on_network_output(name):
                 np.testing.assert_allclose(np.array(row, dtype=np.float64), ref[b, i], atol=1e-4, rtol=1e-4)
 
 
-def test_u8_frames_path_matches_normalized_input():
-    """forward_frames(u8) == forward(Normalize(ToTensor(u8))) (centernet_node.py:90-92)."""
+@pytest.mark.parametrize("precision,name,hw", [("fp32", "r18_c16_b2_96x128", (96, 128)),
+                                               ("fp16", "r18_c16_b2_96x128", (96, 128)),
+                                               ("bf16", "r18_c16_b2_96x128", (96, 128)),
+                                               ("fp16", "torpedo_c16_b1_360x640", (360, 640))])
+def test_u8_frames_path_matches_normalized_input(precision, name, hw):
+    """forward_frames(u8) == forward(Normalize(ToTensor(u8))) (centernet_node.py:90-92), bit for
+    bit: in fp16/bf16 both run through the fused staging + stem kernel (u8 LUT vs fp32 NCHW
+    loads), with partial edge tiles at 360x640."""
     from recipe import seeded_u8_frames, normalize
-    model, oc, mc, case = build("r18_c16_b2_96x128", "fp32")
-    fr = seeded_u8_frames(3, 96, 128, seed=7)
+    model, oc, mc, case = build(name, precision)
+    fr = seeded_u8_frames(3, hw[0], hw[1], seed=7)
     img = normalize(fr.permute(0, 3, 1, 2).float() / 255.0)
     a = model(img.cuda())
     b = model.forward_frames(fr.cuda())

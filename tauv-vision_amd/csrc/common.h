@@ -118,6 +118,24 @@ size_t stem_weight_bytes();
 void stem_fragment_order(const uint16_t* w, int Npad, int Kpad, uint16_t* out);
 int launch_stem(const StemParams& p, int dtype, int grid, hipStream_t s);
 
+// ConvTranspose2d(k = s) + pad_to_match + skip add (convt.hip), fp16/bf16, 128 -> 128 channels.
+struct ConvTParams {
+  const void* src;    // low-res input NHWC [B,h,w,*]
+  int h, w, src_ldc;
+  const void* weight; // packed [s*s*128][Kpad] (row = phase*128 + co)
+  int Kpad;
+  const float* bias;  // [s*s*128]
+  const void* add;    // skip tensor [B,tH,tW,*]
+  int add_ldc;
+  void* out;          // [B,tH,tW,*]
+  int out_ldc;
+  int B, s, tH, tW, sy, sx;
+  int tpw, nchunks;   // schedule (convt_schedule)
+};
+bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc);
+void convt_schedule(ConvTParams& p, int cu_count);
+int launch_convt(const ConvTParams& p, int dtype, hipStream_t s);
+
 // ---- small kernels -----------------------------------------------------------------
 int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad, int dtype,
                      hipStream_t s);

@@ -210,6 +210,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   }
   if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
   // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
   if (stem_mode && dtype != F32)
     for (size_t i = 0; i + 1 < plan.ops.size(); ++i)
@@ -439,6 +440,38 @@ int Engine::make_workspace(int B, Workspace* ws) {
       }
     }
   }
+  // ConvTranspose + pad_to_match + add on convt.hip (fp16/bf16, 128 -> 128 channels)
+  ws->convt.assign(plan.ops.size(), 0);
+  ws->tparams.assign(plan.ops.size(), ConvTParams{});
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    if (!convt_mode || dtype == F32 || op.kind != OP_CONVT_ADD) continue;
+    const TensorSpec& src = plan.tensors[op.src];
+    const TensorSpec& tgt = plan.tensors[op.out];
+    const TensorSpec& add = plan.tensors[op.add];
+    if (!convt_supported(src.C, op.N, src.C, add.C, tgt.C)) continue;
+    ConvTParams& t = ws->tparams[i];
+    t.src = base + ws->off[op.src];
+    t.h = src.H;
+    t.w = src.W;
+    t.src_ldc = src.C;
+    t.weight = packed[i].w;
+    t.Kpad = packed[i].Kpad;
+    t.bias = packed[i].bias;
+    t.add = base + ws->off[op.add];
+    t.add_ldc = add.C;
+    t.out = base + ws->off[op.out];
+    t.out_ldc = tgt.C;
+    t.B = B;
+    t.s = op.up_s;
+    t.tH = tgt.H;
+    t.tW = tgt.W;
+    t.sy = op.sy;
+    t.sx = op.sx;
+    convt_schedule(t, cu_count);
+    ws->convt[i] = 1;
+    ws->use_pipe[i] = 0;
+  }
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
@@ -507,6 +540,16 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     return input_u8 ? launch_prep_u8((const uint8_t*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s)
                     : launch_prep_nchw((const float*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s);
   }
+  if (ws->convt[i]) {
+    int rc = launch_convt(ws->tparams[i], dtype, s);
+    if (rc) return rc;
+    const TensorSpec& tgt = plan.tensors[op.out];
+    const ConvTParams& t = ws->tparams[i];
+    if (op.cov_y0 > 0 || op.cov_x0 > 0 || op.cov_y1 < tgt.H || op.cov_x1 < tgt.W)
+      return launch_uncovered_copy(t.add, t.add_ldc, t.out, t.out_ldc, tgt.C, ws->B, tgt.H, tgt.W, op.cov_y0,
+                                   op.cov_y1, op.cov_x0, op.cov_x1, dtype, s);
+    return TV_OK;
+  }
   ConvParams p = ws->params[i];
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
@@ -564,7 +607,8 @@ const char* Engine::op_kernel(int B, size_t i) {
     const char* o = (op.out < 0) ? "float" : t;
     std::string& name = ws->kname[i];
     if (name.empty()) {
-      if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + o + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ">";
+      if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ">";
+      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + o + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ">";
       else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";

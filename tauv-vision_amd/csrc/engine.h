@@ -29,6 +29,8 @@ struct Workspace {
   std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
   std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
   std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
+  std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
+  std::vector<ConvTParams> tparams; // per op: convt.hip launch parameters
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
   std::vector<unsigned long long*> stamps;  // diagnostics (env TV_STAMPS), per op
   std::vector<std::string> kname;   // per op: kernel instance name (diagnostics), filled lazily
@@ -45,6 +47,7 @@ struct Engine {
   int pipe_mode = -1;          // -1 auto, 0 never, 1 whenever representable (env TV_CONV_PIPE)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
   int cu_count = 256;          // compute units (persistent grids)
+  int convt_mode = 1;          // convt.hip for eligible fp16/bf16 up-paths (env TV_CONVT=0 off)
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1

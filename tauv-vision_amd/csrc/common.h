@@ -69,6 +69,13 @@ struct ConvParams {
   const void* zero;     // >= 16 zero bytes: source of padding taps for LDS-DMA loads
   const KStep* ks;      // pipelined kernel: one descriptor per k-step (nks of them)
   int nks;
+  // conv3x3 EPI = 1 (stacked heads with the block-diagonal 1x1 heads fused, centernet.py:46-61):
+  // N-tile nt's 128 hidden channels feed output columns [head_row0[nt], + head_nrows[nt]) of the
+  // caller's fp32 output (pixel stride head_ldc), accumulated with fp32 atomic adds
+  const void* head_w;   // [ntiles][8 k-steps][64 lanes][16 B] MFMA A-fragments of the 1x1 weights
+  const float* head_b;  // [ntiles][32] 1x1 bias on the first tile of each head, zeros elsewhere
+  int head_ldc;
+  int head_row0[8], head_nrows[8];
   int ablate;           // timing experiments only (env TV_ABLATE): 1 no main-loop DMA, 2 no MFMA
   unsigned long long* stamps;  // diagnostics only (env TV_STAMPS): per block kStampWords words
 };
@@ -92,8 +99,9 @@ int halo_tiles(int B, int H, int W, int tw);
 // tiles of tw (16 or 32) columns; ConvParams.mtiles = conv3x3_tiles(B, H, W, tw); `grid`
 // persistent workgroups (one per CU, a multiple of 8 when >= 8).
 constexpr int kConv3MaxN = 1024;
+// epi = 0: store the activations; epi = 1: fused 1x1 heads into the fp32 output `out` (head_*)
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s);
+                   hipStream_t s, int epi = 0);
 int conv3x3_tiles(int B, int H, int W, int tw);
 // k-step-major, pre-swizzled weight copy the kernel streams (from the [Npad][Kpad] packing)
 size_t conv3x3_weight_bytes(int ntiles);

@@ -119,7 +119,7 @@ __device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh
   gstore16(dst + 8 * lh, make_uint4(r0[0], r1[0], r0[1], r1[1]));
 }
 
-template <typename T, typename OutT, int TW, int ACT>
+template <typename T, typename OutT, int TW, int ACT, int EPI>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
   constexpr int TH = P / TW;
@@ -287,6 +287,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       const bool ok = y < H && x < W;
       OutT* dst = reinterpret_cast<OutT*>(out_ptr) +
                   ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.out_ldc + p.out_coff + n0;
+      [[maybe_unused]] f32x16 hacc = f32x16{};  // EPI 1: the 1x1 heads' partial sums of this pixel
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -304,10 +305,37 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
               v[gg][e] = t;
             }
           }
-          const int ch = n0 + 32 * i + 16 * m;
-          if (ok && ch < p.N) store_out<OutT>(dst + 32 * i + 16 * m, v, lh);
+          if constexpr (EPI == 0) {
+            const int ch = n0 + 32 * i + 16 * m;
+            if (ok && ch < p.N) store_out<OutT>(dst + 32 * i + 16 * m, v, lh);
+          } else {
+            // the 8 hidden channels 32i+16m+8lh.. of this pixel, rounded to T exactly as the
+            // unfused path stores them, are the MFMA B operand of k-step 2i+m of the 1x1
+            const unsigned a0 = pack2<T>(v[0][0], v[0][1]), a1 = pack2<T>(v[0][2], v[0][3]);
+            const unsigned b0 = pack2<T>(v[1][0], v[1][1]), b1 = pack2<T>(v[1][2], v[1][3]);
+            const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            const uint4 hv = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+            const uint4 hwf = gload16(reinterpret_cast<const char*>(p.head_w) +
+                                      ((size_t)(nt * 8 + 2 * i + m) * 64 + lane) * 16);
+            Mfma<T>::run(hwf, hv, hacc);
+          }
           __builtin_amdgcn_sched_barrier(0);  // bound the live set: one 8-channel group at a time
         }
+      }
+      if constexpr (EPI == 1) {
+        // rows r = 8G + 4lh + e of the 1x1 result: output column head_row0[nt] + r of pixel (y, x)
+        const int nr = p.head_nrows[nt];
+        float* hd = reinterpret_cast<float*>(out_ptr) + ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.head_ldc +
+                    p.head_row0[nt];
+        const float* hb = p.head_b + nt * 32;
+#pragma unroll
+        for (int G = 0; G < 4; ++G)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * G + 4 * lh + e;
+            if (ok && r < nr) unsafeAtomicAdd(hd + r, hacc[4 * G + e] + hb[r]);
+          }
       }
     }
   };
@@ -480,9 +508,9 @@ __global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntil
   }
 }
 
-template <typename T, int TW, int ACT>
+template <typename T, int TW, int ACT, int EPI = 0>
 static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
-  auto k = conv3x3<T, T, TW, ACT>;
+  auto k = conv3x3<T, T, TW, ACT, EPI>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -518,10 +546,20 @@ int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, void* out, hipS
 }
 
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s) {
+                   hipStream_t s, int epi) {
   using namespace c3;
   if (p.act < 0 || p.act > 2) {
     set_error("conv3x3: bad activation");
+    return 1;
+  }
+  if (epi == 1) {  // fused 1x1 heads: the stacked heads' LeakyReLU only
+    if (p.act != 2 || p.ntiles > 8) {
+      set_error("conv3x3: fused heads need LeakyReLU and <= 8 channel tiles");
+      return 1;
+    }
+    if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 2, 1>(p, dp, out, grid, s) : launch_t<_Float16, 16, 2, 1>(p, dp, out, grid, s);
+    if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 2, 1>(p, dp, out, grid, s) : launch_t<__bf16, 16, 2, 1>(p, dp, out, grid, s);
+    set_error("conv3x3: fp16/bf16 only");
     return 1;
   }
   using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);

@@ -168,6 +168,39 @@ int Engine::pack_op(size_t oi) {
       }
     }
   }
+  // fused 1x1 heads (conv3x3 EPI 1): per 128-channel tile nt of the hidden (stacked 3x3) output,
+  // fragment (k-step j, lane l) = 8 weights W2[row0 + l%32][128nt + 16j + 8(l/32) + e]
+  if (dtype != F32 && !op.diag_in_off.empty() && op.segs.size() == 1) {
+    const int K = plan.tensors[op.segs[0].src].C;  // hidden channels
+    const int nts = K / 128;
+    const int hid = K / (int)op.stack_w.size();    // hidden channels per head
+    bool ok = K % 128 == 0 && nts <= 8 && hid % 128 == 0;
+    for (size_t h = 0; h < op.stack_n.size(); ++h) ok = ok && op.stack_n[h] <= 32;
+    if (ok) {
+      std::vector<uint8_t> frag((size_t)nts * 8 * 64 * 16, 0);
+      std::vector<float> hb((size_t)nts * 32, 0.f);
+      for (int nt = 0; nt < nts; ++nt) {
+        const int h = nt * 128 / hid;
+        const int row0 = op.diag_out_off[h], nr = op.stack_n[h];
+        pk.head_row0[nt] = row0;
+        pk.head_nrows[nt] = nr;
+        if (nt * 128 == op.diag_in_off[h])
+          for (int r = 0; r < nr; ++r) hb[nt * 32 + r] = bias[row0 + r];
+        for (int j = 0; j < 8; ++j)
+          for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 8; ++e) {
+              const int r = l & 31, k = nt * 128 + 16 * j + 8 * (l >> 5) + e;
+              const float v = r < nr ? hw[(size_t)(row0 + r) * pk.Kpad + k] : 0.f;
+              store_elem(frag.data(), ((size_t)(nt * 8 + j) * 64 + l) * 8 + e, v, dtype);
+            }
+      }
+      TV_HIP(hipMalloc(&pk.head_w, frag.size()));
+      TV_HIP(hipMemcpy(pk.head_w, frag.data(), frag.size(), hipMemcpyHostToDevice));
+      TV_HIP(hipMalloc((void**)&pk.head_b, hb.size() * sizeof(float)));
+      TV_HIP(hipMemcpy(pk.head_b, hb.data(), hb.size() * sizeof(float), hipMemcpyHostToDevice));
+      pk.head_ok = 1;
+    }
+  }
   // device copies
   std::vector<uint8_t> hbuf((size_t)pk.Npad * pk.Kpad * esz);
   for (size_t i = 0; i < hw.size(); ++i) store_elem(hbuf.data(), i, hw[i], dtype);
@@ -211,6 +244,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
   // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
   if (stem_mode && dtype != F32)
     for (size_t i = 0; i + 1 < plan.ops.size(); ++i)
@@ -234,6 +268,8 @@ Engine::~Engine() {
   for (auto& p : packed) {
     if (p.w) (void)hipFree(p.w);
     if (p.w_c3) (void)hipFree(p.w_c3);
+    if (p.head_w) (void)hipFree(p.head_w);
+    if (p.head_b) (void)hipFree(p.head_b);
     if (p.bias) (void)hipFree(p.bias);
   }
   for (auto& kv : workspaces) {
@@ -440,6 +476,26 @@ int Engine::make_workspace(int B, Workspace* ws) {
       }
     }
   }
+  // stacked 3x3 heads on conv3x3 + block-diagonal 1x1 heads -> one launch (EPI 1)
+  ws->head_fused.assign(plan.ops.size(), 0);
+  ws->head_skip.assign(plan.ops.size(), 0);
+  for (size_t i = 0; headfuse_mode && i + 1 < plan.ops.size(); ++i) {
+    const OpSpec& h2 = plan.ops[i + 1];
+    const Packed& pk2 = packed[i + 1];
+    if (!ws->c3_tw[i] || h2.diag_in_off.empty() || !pk2.head_ok || h2.out >= 0 || h2.segs[0].src != plan.ops[i].out ||
+        plan.ops[i].act != 2 || ws->params[i].ntiles != plan.ops[i].N / 128)
+      continue;
+    ConvParams& p = ws->params[i];
+    p.head_w = pk2.head_w;
+    p.head_b = pk2.head_b;
+    p.head_ldc = plan.out_cpad;
+    for (int t = 0; t < 8; ++t) {
+      p.head_row0[t] = pk2.head_row0[t];
+      p.head_nrows[t] = pk2.head_nrows[t];
+    }
+    ws->head_fused[i] = 1;
+    ws->head_skip[i + 1] = 1;
+  }
   // ConvTranspose + pad_to_match + add on convt.hip (fp16/bf16, 128 -> 128 channels)
   ws->convt.assign(plan.ops.size(), 0);
   ws->tparams.assign(plan.ops.size(), ConvTParams{});
@@ -540,6 +596,11 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     return input_u8 ? launch_prep_u8((const uint8_t*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s)
                     : launch_prep_nchw((const float*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s);
   }
+  if (ws->head_skip[i]) return TV_OK;  // fused into the 3x3 heads launch
+  if (ws->head_fused[i]) {
+    TV_HIP(hipMemsetAsync(out, 0, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad * sizeof(float), s));
+    return launch_conv3x3(ws->params[i], ws->dparams + i, out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 1);
+  }
   if (ws->convt[i]) {
     int rc = launch_convt(ws->tparams[i], dtype, s);
     if (rc) return rc;
@@ -608,7 +669,8 @@ const char* Engine::op_kernel(int B, size_t i) {
     std::string& name = ws->kname[i];
     if (name.empty()) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ">";
-      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + o + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ">";
+      else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
+      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ">";
       else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";

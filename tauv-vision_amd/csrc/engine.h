@@ -17,6 +17,12 @@ struct Packed {
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;
+  // block-diagonal 1x1 heads only: MFMA A-fragments per 128-channel tile of the stacked 3x3
+  // heads' output, for the fused epilogue (conv3x3 EPI 1); head_ok = 0 when not representable
+  int head_ok = 0;
+  void* head_w = nullptr;
+  float* head_b = nullptr;
+  int head_row0[8] = {}, head_nrows[8] = {};
 };
 
 struct Workspace {
@@ -29,6 +35,8 @@ struct Workspace {
   std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
   std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
   std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
+  std::vector<int> head_fused;      // per op: 1 = stacked 3x3 heads with the 1x1 heads fused in
+  std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
   std::vector<ConvTParams> tparams; // per op: convt.hip launch parameters
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
@@ -47,6 +55,7 @@ struct Engine {
   int pipe_mode = -1;          // -1 auto, 0 never, 1 whenever representable (env TV_CONV_PIPE)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
   int cu_count = 256;          // compute units (persistent grids)
+  int headfuse_mode = 1;       // fuse the 1x1 heads into the 3x3 heads epilogue (env TV_HEADFUSE=0 off)
   int convt_mode = 1;          // convt.hip for eligible fp16/bf16 up-paths (env TV_CONVT=0 off)
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)

@@ -101,8 +101,7 @@ int tv_engine_destroy(tv_engine* e) {
 int tv_engine_prepare(tv_engine* e, int32_t B, void* stream) {
   TV_GUARD({
     if (!e || B < 1) { set_error("bad argument"); return TV_EINVAL; }
-    Workspace* ws;
-    return e->e.get_workspace(B, (hipStream_t)stream, &ws);
+    return e->e.prepare(B, (hipStream_t)stream);
   })
 }
 

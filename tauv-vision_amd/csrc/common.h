@@ -139,6 +139,9 @@ struct ConvTParams {
   int out_ldc;
   int B, s, tH, tW, sy, sx;
   int tpw, nchunks;   // schedule (convt_schedule)
+  int mode;           // 0: ConvTranspose + add; 1: 1x1 conv, out (b,oy,ox) <- src (b,oy*stride,ox*stride);
+                      // 2: mode 1 + add[b,oy,ox] before the activation
+  int stride, act;    // modes 1, 2
 };
 bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc);
 void convt_schedule(ConvTParams& p, int cu_count);

@@ -18,6 +18,12 @@
 //  * the epilogue works on the accumulators in place (bias, + skip in fp32, one rounding,
 //    v_permlane32_swap into 16-byte stores), in the same arithmetic order as conv_pipe's
 //    mode-1 epilogue: (acc + bias) + skip.
+//
+// MODE 1 reuses the same machinery for a 1x1 convolution with stride: output pixel (b, oy, ox)
+// reads input pixel (b, oy*stride, ox*stride); optional ReLU. MODE 2 is MODE 1 plus a tensor
+// added at the output pixel before the ReLU: ResidualBlock's tail relu(bn2(conv2(y)) +
+// bn_residual(conv_residual(x))) (dla.py:39-52) when the planner splits the 1x1 residual out of
+// conv2's GEMM (conv2 then runs on the 3x3 halo kernel and stores bn2(conv2(y)) unactivated).
 #include "conv_common.h"
 
 namespace tv {
@@ -49,7 +55,7 @@ struct Set {
   uint4 a[8];    // skip chunks (i, m): channels 32i + 16m + 8*lh .. +8 at the target pixel
 };
 
-template <typename T>
+template <typename T, int MODE>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void convt_add(ConvTParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -73,7 +79,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   __syncthreads();
 
-  const int hw = p.h * p.w;
+  // MODE 0: GEMM rows are input pixels (b, iy, ix); MODE 1: output pixels (b, oy, ox)
+  const int hw = MODE == 0 ? p.h * p.w : p.tH * p.tW;
   const int M = p.B * hw;
   const int mt = (M + 31) / 32;
   const int t_begin = (chunk * 4 + wave) * p.tpw;
@@ -84,6 +91,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto target = [&](int t) __attribute__((always_inline)) -> long long {
     const int m = t * 32 + l32;
     if (m >= M) return -1;
+    if constexpr (MODE != 0) return m;
     const int b = m / hw;
     const int rem = m - b * hw;
     const int iy = rem / p.w, ix = rem - iy * p.w;
@@ -93,10 +101,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
   auto load = [&](int t, Set& S) __attribute__((always_inline)) {
     const int m = t * 32 + l32;
-    const T* src = reinterpret_cast<const T*>(p.src) + (size_t)(m < M ? m : 0) * p.src_ldc + 8 * lh;
+    size_t sp = (size_t)(m < M ? m : 0);
+    if constexpr (MODE != 0) {  // strided 1x1: input pixel (b, oy*stride, ox*stride)
+      const int b = (int)sp / hw;
+      const int rem = (int)sp - b * hw;
+      const int oy = rem / p.tW, ox = rem - oy * p.tW;
+      sp = ((size_t)(b * p.h + oy * p.stride)) * p.w + (size_t)ox * p.stride;
+    }
+    const T* src = reinterpret_cast<const T*>(p.src) + sp * p.src_ldc + 8 * lh;
 #pragma unroll
     for (int j = 0; j < KJ; ++j) S.x[j] = gload16(src + 16 * j);
-    const long long tg = target(t);
+    if constexpr (MODE == 1) return;
+    const long long tg = target(t);  // MODE 2: the output pixel itself
     const T* add = reinterpret_cast<const T*>(p.add) + (tg < 0 ? 0 : tg) * p.add_ldc + 8 * lh;
 #pragma unroll
     for (int q = 0; q < 8; ++q) S.a[q] = gload16(add + 16 * q);  // q = 2i + m -> channel 16q + 8lh
@@ -146,11 +162,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         const float f[8] = {__uint_as_float(r0[0]), __uint_as_float(r1[0]), __uint_as_float(r2[0]),
                             __uint_as_float(r3[0]), __uint_as_float(r0[1]), __uint_as_float(r1[1]),
                             __uint_as_float(r2[1]), __uint_as_float(r3[1])};
-        const uint4 sk = S.a[2 * i + m];
-        const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
         unsigned o[4];
+        if constexpr (MODE != 1) {
+          const uint4 sk = S.a[2 * i + m];
+          const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = pack2<T>(lo_f<T>(sw[e]) + f[2 * e], hi_f<T>(sw[e]) + f[2 * e + 1]);
+          for (int e = 0; e < 4; ++e) {
+            float u0 = lo_f<T>(sw[e]) + f[2 * e], u1 = hi_f<T>(sw[e]) + f[2 * e + 1];
+            if (MODE == 2 && p.act == 1) u0 = fmaxf(u0, 0.0f), u1 = fmaxf(u1, 0.0f);
+            o[e] = pack2<T>(u0, u1);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float u0 = f[2 * e], u1 = f[2 * e + 1];
+            if (p.act == 1) u0 = fmaxf(u0, 0.0f), u1 = fmaxf(u1, 0.0f);
+            o[e] = pack2<T>(u0, u1);
+          }
+        }
         if (tg >= 0) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
       }
   };
@@ -167,9 +196,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 }
 
-template <typename T>
+template <typename T, int MODE>
 static int launch_t(const ConvTParams& p, hipStream_t s) {
-  auto k = convt_add<T>;
+  auto k = convt_add<T, MODE>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -179,7 +208,7 @@ static int launch_t(const ConvTParams& p, hipStream_t s) {
     }
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(p.s * p.s * p.nchunks), dim3(NT), LDS, s, p);
+  hipLaunchKernelGGL(k, dim3((MODE == 0 ? p.s * p.s : 1) * p.nchunks), dim3(NT), LDS, s, p);
   TV_HIP(hipGetLastError());
   return 0;
 }
@@ -192,7 +221,8 @@ bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc) {
 
 // tiles per wave: about 2 resident workgroups (8 waves) per CU over the whole launch, at least 4 tiles per wave
 void convt_schedule(ConvTParams& p, int cu_count) {
-  const long M = (long)p.B * p.h * p.w;
+  if (p.mode != 0) p.s = 1;  // one "phase"
+  const long M = (long)p.B * (p.mode != 0 ? (long)p.tH * p.tW : (long)p.h * p.w);
   const long mt = (M + 31) / 32;
   const long waves_target = 2L * 4 * cu_count;  // 2 workgroups x 4 waves per CU
   long per_phase = (waves_target + p.s * p.s - 1) / (p.s * p.s);
@@ -207,8 +237,15 @@ int launch_convt(const ConvTParams& p, int dtype, hipStream_t s) {
     set_error("convt: not scheduled");
     return 1;
   }
-  if (dtype == F16) return convt::launch_t<_Float16>(p, s);
-  if (dtype == BF16) return convt::launch_t<__bf16>(p, s);
+  using L = int (*)(const ConvTParams&, hipStream_t);
+  static const L f16[3] = {convt::launch_t<_Float16, 0>, convt::launch_t<_Float16, 1>, convt::launch_t<_Float16, 2>};
+  static const L b16[3] = {convt::launch_t<__bf16, 0>, convt::launch_t<__bf16, 1>, convt::launch_t<__bf16, 2>};
+  if (p.mode < 0 || p.mode > 2) {
+    set_error("convt: bad mode");
+    return 1;
+  }
+  if (dtype == F16) return f16[p.mode](p, s);
+  if (dtype == BF16) return b16[p.mode](p, s);
   set_error("convt: fp16/bf16 only");
   return 1;
 }

@@ -245,6 +245,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_SLICES")) slices = std::atoi(env);
   // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
   if (stem_mode && dtype != F32)
     for (size_t i = 0; i + 1 < plan.ops.size(); ++i)
@@ -278,6 +279,11 @@ Engine::~Engine() {
     if (kv.second->dks) (void)hipFree(kv.second->dks);
     delete kv.second;
   }
+  for (auto& kv : side) {
+    if (kv.second.fork) (void)hipEventDestroy(kv.second.fork);
+    if (kv.second.join) (void)hipEventDestroy(kv.second.join);
+    if (kv.second.s) (void)hipStreamDestroy(kv.second.s);
+  }
 }
 
 // Liveness-planned arena: a tensor lives from its producing op to its last reader;
@@ -290,10 +296,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
     const OpSpec& op = plan.ops[i];
     if (op.out >= 0) def[op.out] = (int)i, last[op.out] = std::max(last[op.out], (int)i);
     for (const SegSpec& s : op.segs) last[s.src] = std::max(last[s.src], (int)i);
-    if (op.kind == OP_CONVT_ADD) {
-      last[op.src] = std::max(last[op.src], (int)i);
-      last[op.add] = std::max(last[op.add], (int)i);
-    }
+    if (op.kind == OP_CONVT_ADD) last[op.src] = std::max(last[op.src], (int)i);
+    if (op.add >= 0) last[op.add] = std::max(last[op.add], (int)i);
   }
   ws->off.assign(nt, 0);
   struct Live { size_t off, size; int last; };
@@ -501,6 +505,41 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->tparams.assign(plan.ops.size(), ConvTParams{});
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
+    if (op.kind == OP_CONV && op.add >= 0) {
+      // split ResidualBlock tail: residual 1x1 GEMM + add + ReLU (convt.hip mode 2)
+      const SegSpec& sg = op.segs[0];
+      const TensorSpec& src = plan.tensors[sg.src];
+      const TensorSpec& tgt = plan.tensors[op.out];
+      const TensorSpec& add = plan.tensors[op.add];
+      if (dtype == F32 || op.segs.size() != 1 || sg.kh != 1 || sg.kw != 1 || sg.pad != 0 ||
+          !convt_supported(src.C, op.N, src.C, add.C, tgt.C)) {
+        set_error("residual tail " + op.label + ": no kernel for this shape");
+        return TV_ESHAPE;
+      }
+      ConvTParams& t = ws->tparams[i];
+      t.mode = 2;
+      t.src = base + ws->off[sg.src];
+      t.h = src.H;
+      t.w = src.W;
+      t.src_ldc = src.C;
+      t.stride = sg.stride;
+      t.act = op.act;
+      t.weight = packed[i].w;
+      t.Kpad = packed[i].Kpad;
+      t.bias = packed[i].bias;
+      t.add = base + ws->off[op.add];
+      t.add_ldc = add.C;
+      t.out = base + ws->off[op.out];
+      t.out_ldc = tgt.C;
+      t.B = B;
+      t.tH = tgt.H;
+      t.tW = tgt.W;
+      convt_schedule(t, cu_count);
+      ws->convt[i] = 1;
+      ws->use_pipe[i] = 0;
+      ws->c3_tw[i] = 0;
+      continue;
+    }
     if (!convt_mode || dtype == F32 || op.kind != OP_CONVT_ADD) continue;
     const TensorSpec& src = plan.tensors[op.src];
     const TensorSpec& tgt = plan.tensors[op.out];
@@ -603,7 +642,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   }
   if (ws->convt[i]) {
     int rc = launch_convt(ws->tparams[i], dtype, s);
-    if (rc) return rc;
+    if (rc || op.kind != OP_CONVT_ADD) return rc;
     const TensorSpec& tgt = plan.tensors[op.out];
     const ConvTParams& t = ws->tparams[i];
     if (op.cov_y0 > 0 || op.cov_x0 > 0 || op.cov_y1 < tgt.H || op.cov_x1 < tgt.W)
@@ -629,6 +668,46 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   return TV_OK;
 }
 
+int Engine::get_side(hipStream_t s, SideStream** out) {
+  std::lock_guard<std::mutex> g(mu);
+  auto it = side.find((void*)s);
+  if (it == side.end()) {
+    SideStream ss;
+    TV_HIP(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
+    TV_HIP(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
+    TV_HIP(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
+    it = side.emplace((void*)s, ss).first;
+  }
+  *out = &it->second;
+  return TV_OK;
+}
+
+int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStream_t s) {
+  Workspace* ws = nullptr;
+  int rc = get_workspace(B, s, &ws);
+  if (rc) return rc;
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    rc = run_op(i, ws, input, input_u8, out, s);
+    if (rc) return rc;
+  }
+  return TV_OK;
+}
+
+int Engine::prepare(int B, hipStream_t s) {
+  TV_HIP(hipSetDevice(device));
+  if (slices > 1 && B >= 2 * slice_min) {
+    SideStream* ss = nullptr;
+    int rc = get_side(s, &ss);
+    if (rc) return rc;
+    Workspace* ws = nullptr;
+    rc = get_workspace(B / 2, s, &ws);
+    if (rc) return rc;
+    return get_workspace(B - B / 2, ss->s, &ws);
+  }
+  Workspace* ws = nullptr;
+  return get_workspace(B, s, &ws);
+}
+
 int Engine::forward(const void* input, int input_u8, int B, float* out, hipStream_t s) {
   if (B < 1) {
     set_error("batch must be >= 1");
@@ -639,14 +718,26 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
     return TV_EINVAL;
   }
   TV_HIP(hipSetDevice(device));
-  Workspace* ws = nullptr;
-  int rc = get_workspace(B, s, &ws);
-  if (rc) return rc;
-  for (size_t i = 0; i < plan.ops.size(); ++i) {
-    rc = run_op(i, ws, input, input_u8, out, s);
+  if (slices > 1 && B >= 2 * slice_min) {
+    // frames are independent (no cross-frame state): first half on `s`, second on the side
+    // stream, joined back into `s` (graph-capture safe: event fork / join)
+    SideStream* ss = nullptr;
+    int rc = get_side(s, &ss);
     if (rc) return rc;
+    const int B1 = B / 2;
+    const size_t in_frame = input_u8 ? (size_t)desc.in_h * desc.in_w * 3 : (size_t)3 * desc.in_h * desc.in_w * 4;
+    const size_t out_frame = (size_t)plan.out_h * plan.out_w * plan.out_cpad;
+    TV_HIP(hipEventRecord(ss->fork, s));
+    TV_HIP(hipStreamWaitEvent(ss->s, ss->fork, 0));
+    rc = run_all(input, input_u8, B1, out, s);
+    if (rc) return rc;
+    rc = run_all((const char*)input + B1 * in_frame, input_u8, B - B1, out + B1 * out_frame, ss->s);
+    if (rc) return rc;
+    TV_HIP(hipEventRecord(ss->join, ss->s));
+    TV_HIP(hipStreamWaitEvent(s, ss->join, 0));
+    return TV_OK;
   }
-  return TV_OK;
+  return run_all(input, input_u8, B, out, s);
 }
 
 const char* Engine::op_kernel(int B, size_t i) {
@@ -668,7 +759,7 @@ const char* Engine::op_kernel(int B, size_t i) {
     const char* o = (op.out < 0) ? "float" : t;
     std::string& name = ws->kname[i];
     if (name.empty()) {
-      if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ">";
+      if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].mode) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ">";
       else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";

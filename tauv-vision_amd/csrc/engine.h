@@ -52,7 +52,7 @@ struct Engine {
   std::vector<Packed> packed;  // per op
   size_t weight_bytes = 0;
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
-  int pipe_mode = -1;          // -1 auto, 0 never, 1 whenever representable (env TV_CONV_PIPE)
+  int pipe_mode = 1;           // -1 auto (>= 256 tiles), 0 never, 1 whenever representable (env TV_CONV_PIPE)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
   int cu_count = 256;          // compute units (persistent grids)
   int headfuse_mode = 1;       // fuse the 1x1 heads into the 3x3 heads epilogue (env TV_HEADFUSE=0 off)
@@ -61,6 +61,16 @@ struct Engine {
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1
   int halo_mode = 0;           // 1 enables the halo-tile 3x3 kernel, 2 forces it (env TV_CONV_HALO)
+  // concurrent slices: a batch of >= 2 * slice_min frames runs as two halves on the caller's
+  // stream and a side stream (fork / join events), so one half's latency-bound small layers
+  // overlap the other half's large ones (env TV_SLICES=1 off)
+  int slices = 2;
+  int slice_min = 8;
+  struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+  };
+  std::map<void*, SideStream> side;  // per caller stream
   std::mutex mu;
   std::map<std::pair<void*, int>, Workspace*> workspaces;
   std::unordered_map<std::string, std::pair<const float*, int64_t>> host_w;  // during create only
@@ -68,6 +78,7 @@ struct Engine {
   ~Engine();
   int create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev);
   int get_workspace(int B, hipStream_t s, Workspace** out);
+  int prepare(int B, hipStream_t s);  // workspaces (and side stream) for forward(B) on s
   int forward(const void* input, int input_u8, int B, float* out, hipStream_t s);
   int profile(const void* input, int input_u8, int B, float* out, hipStream_t s, float* ms, double* flops, int cap, int* n_ops);
   const char* op_kernel(int B, size_t i);
@@ -79,6 +90,8 @@ struct Engine {
   int pack_op(size_t i);
   int make_workspace(int B, Workspace* ws);
   int run_op(size_t i, Workspace* ws, const void* input, int input_u8, float* out, hipStream_t s);
+  int run_all(const void* input, int input_u8, int B, float* out, hipStream_t s);
+  int get_side(hipStream_t s, SideStream** out);
 };
 
 }  // namespace tv

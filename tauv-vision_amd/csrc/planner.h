@@ -42,7 +42,7 @@ struct OpSpec {
   // final block-diagonal 1x1 heads: weight j feeds output channels [out_off[j], +n) from
   // input channels [in_off[j], +cin)
   std::vector<int> diag_in_off, diag_out_off;
-  // OP_CONVT_ADD
+  // OP_CONVT_ADD (and OP_CONV: `add` >= 0 = tensor added before the activation)
   int src = -1, add = -1, up_s = 0, sy = 0, sx = 0;
   std::string up_w;           // ConvTranspose2d prefix
   int cov_y0 = 0, cov_y1 = 0, cov_x0 = 0, cov_x1 = 0;  // covered target rectangle

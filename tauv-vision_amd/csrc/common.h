@@ -138,10 +138,11 @@ struct ConvTParams {
   void* out;          // [B,tH,tW,*]
   int out_ldc;
   int B, s, tH, tW, sy, sx;
-  int tpw, nchunks;   // schedule (convt_schedule)
+  int tpw, nchunks, np;  // schedule (convt_schedule): tiles per wave, workgroups per phase group, phases per group
   int mode;           // 0: ConvTranspose + add; 1: 1x1 conv, out (b,oy,ox) <- src (b,oy*stride,ox*stride);
                       // 2: mode 1 + add[b,oy,ox] before the activation
   int stride, act;    // modes 1, 2
+  int ablate;         // timing experiments only (env TV_CONVT_ABLATE): 1 no stores, 2 no MFMA, 4 no skip loads
 };
 bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc);
 void convt_schedule(ConvTParams& p, int cu_count);

@@ -29,12 +29,15 @@
 namespace tv {
 namespace convt {
 
-constexpr int NT = 256;        // 4 waves
+constexpr int NT = 512;        // 8 waves
+constexpr int NW = NT / 64;
 constexpr int C = 128;         // output channels per phase (4 MFMA row tiles)
 constexpr int KJ = 8;          // K = 128 input channels = 8 MFMA k-steps of 16
 constexpr int WPITCH = 272;    // LDS weight row pitch (bytes): odd multiple of 16 -> no bank conflicts
-constexpr int OFF_B = C * WPITCH;
-constexpr int LDS = OFF_B + C * 4;
+constexpr int PW = C * WPITCH; // one phase's weights
+constexpr int NPG = 4;         // phases per workgroup (MODE 0): the input tile is loaded once for all
+template <int NP>
+constexpr int lds_bytes() { return NP * (PW + C * 4); }
 
 template <typename T>
 __device__ __forceinline__ unsigned pack2(float a, float b) {
@@ -50,48 +53,57 @@ __device__ __forceinline__ float hi_f(unsigned u) {
   return (float)__builtin_bit_cast(T, (uint16_t)(u >> 16));
 }
 
-struct Set {
+struct XSet {
   uint4 x[KJ];   // B operand: input pixel channels 16j + 8*lh .. +8
-  uint4 a[8];    // skip chunks (i, m): channels 32i + 16m + 8*lh .. +8 at the target pixel
+};
+struct ASet {
+  uint4 a[8];    // skip / residual chunks (i, m): channels 32i + 16m + 8*lh .. +8 at the target pixel
 };
 
-template <typename T, int MODE>
+// MODE 0: a workgroup owns NP consecutive phases of the s*s and a run of 32-pixel input tiles;
+// per tile a wave loads the input operand once and runs the NP phases, the skip chunks of the
+// next phase step in flight under the current one (NP = 4 on large inputs; NP = 1 spreads
+// small inputs over s*s times more workgroups). MODES 1, 2: NP = 1.
+template <typename T, int MODE, int NP>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void convt_add(ConvTParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(NP == 1 || (MODE == 0 && NP % 2 == 0), "phase group");
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, lh = lane >> 5;
-  const int phase = blockIdx.x / p.nchunks;
-  const int chunk = blockIdx.x - phase * p.nchunks;
-  const int py = phase / p.s, px = phase - py * p.s;
+  const int group = blockIdx.x / p.nchunks;
+  const int chunk = blockIdx.x - group * p.nchunks;
+  const int phase0 = group * NP;
 
-  // ---- the phase's weights and bias into LDS (rows n = phase*C + co of the packed [N][Kpad])
+  // ---- the group's weights and bias into LDS (rows n = phase*C + co of the packed [N][Kpad])
   {
-    const char* wsrc = reinterpret_cast<const char*>(p.weight) + (size_t)phase * C * p.Kpad * sizeof(T);
-    for (int i = tid; i < C * 16; i += NT) {
-      const int r = i >> 4, c = i & 15;
+    const char* wsrc = reinterpret_cast<const char*>(p.weight) + (size_t)phase0 * C * p.Kpad * sizeof(T);
+    for (int i = tid; i < NP * C * 16; i += NT) {
+      const int r = i >> 4, c = i & 15;  // r = phase-in-group * C + co
       *reinterpret_cast<uint4*>(smem + r * WPITCH + c * 16) =
           *reinterpret_cast<const uint4*>(wsrc + (size_t)r * p.Kpad * sizeof(T) + c * 16);
     }
-    float* lb = reinterpret_cast<float*>(smem + OFF_B);
-    if (tid < C) lb[tid] = p.bias[phase * C + tid];
+    float* lb = reinterpret_cast<float*>(smem + NP * PW);
+    for (int i = tid; i < NP * C; i += NT) lb[i] = p.bias[phase0 * C + i];
   }
   __syncthreads();
 
-  // MODE 0: GEMM rows are input pixels (b, iy, ix); MODE 1: output pixels (b, oy, ox)
+  // MODE 0: GEMM rows are input pixels (b, iy, ix); MODES 1, 2: output pixels (b, oy, ox)
   const int hw = MODE == 0 ? p.h * p.w : p.tH * p.tW;
   const int M = p.B * hw;
   const int mt = (M + 31) / 32;
-  const int t_begin = (chunk * 4 + wave) * p.tpw;
+  const int t_begin = (chunk * NW + wave) * p.tpw;
   const int t_end = min(t_begin + p.tpw, mt);
   if (t_begin >= t_end) return;
 
-  // target element offset (channel 0) of this lane's pixel in tile t, or -1
-  auto target = [&](int t) __attribute__((always_inline)) -> long long {
+  // target element offset (channel 0) of this lane's pixel in tile t for phase ph, or -1
+  auto target = [&](int t, int ph) __attribute__((always_inline)) -> long long {
     const int m = t * 32 + l32;
     if (m >= M) return -1;
     if constexpr (MODE != 0) return m;
+    const int phase = phase0 + ph;
+    const int py = phase / p.s, px = phase - py * p.s;
     const int b = m / hw;
     const int rem = m - b * hw;
     const int iy = rem / p.w, ix = rem - iy * p.w;
@@ -99,7 +111,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     if (Y >= p.tH || X >= p.tW) return -1;
     return ((long long)(b * p.tH + Y) * p.tW + X);
   };
-  auto load = [&](int t, Set& S) __attribute__((always_inline)) {
+  auto load_x = [&](int t, XSet& S) __attribute__((always_inline)) {
     const int m = t * 32 + l32;
     size_t sp = (size_t)(m < M ? m : 0);
     if constexpr (MODE != 0) {  // strided 1x1: input pixel (b, oy*stride, ox*stride)
@@ -111,31 +123,34 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const T* src = reinterpret_cast<const T*>(p.src) + sp * p.src_ldc + 8 * lh;
 #pragma unroll
     for (int j = 0; j < KJ; ++j) S.x[j] = gload16(src + 16 * j);
-    if constexpr (MODE == 1) return;
-    const long long tg = target(t);  // MODE 2: the output pixel itself
+  };
+  auto load_a = [&](int t, int ph, ASet& S) __attribute__((always_inline)) {
+    if (MODE == 1 || (p.ablate & 4)) return;
+    const long long tg = target(t, ph);  // MODE 2: the output pixel itself
     const T* add = reinterpret_cast<const T*>(p.add) + (tg < 0 ? 0 : tg) * p.add_ldc + 8 * lh;
 #pragma unroll
     for (int q = 0; q < 8; ++q) S.a[q] = gload16(add + 16 * q);  // q = 2i + m -> channel 16q + 8lh
   };
 
-  const char* wl = smem + l32 * WPITCH + lh * 16;
-  const float* lb = reinterpret_cast<const float*>(smem + OFF_B);
-  auto compute_store = [&](int t, const Set& S) __attribute__((always_inline)) {
+  auto compute_store = [&](int t, int ph, const XSet& X, const ASet& A) __attribute__((always_inline)) {
+    const char* wl = smem + ph * PW + l32 * WPITCH + lh * 16;
+    const float* lb = reinterpret_cast<const float*>(smem + NP * PW) + ph * C;
     f32x16 acc[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
-    // weight fragments one k-step at a time (bounded live set: the two register sets, the
-    // accumulators and 16 fragment registers)
+    // weight fragments one k-step at a time (bounded live set)
 #pragma unroll
     for (int j = 0; j < KJ; ++j) {
       uint4 wv[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) wv[i] = *reinterpret_cast<const uint4*>(wl + i * 32 * WPITCH + j * 32);
+      if (!(p.ablate & 2)) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Mfma<T>::run(wv[i], S.x[j], acc[i]);
+        for (int i = 0; i < 4; ++i) Mfma<T>::run(wv[i], X.x[j], acc[i]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
-    const long long tg = target(t);
+    const long long tg = target(t, ph);
     T* out = reinterpret_cast<T*>(p.out) + (tg < 0 ? 0 : tg) * p.out_ldc;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -150,21 +165,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
           for (int e = 0; e < 4; ++e) v[gg][e] = acc[i][4 * G2 + e] + bb[e];
         }
         // registers -> 16-byte chunk: lanes 0-31 channels 32i+16m+0..7, lanes 32-63 +8..15
-        const unsigned a0 = __float_as_uint(v[0][0]), a1 = __float_as_uint(v[0][1]);
-        const unsigned a2 = __float_as_uint(v[0][2]), a3 = __float_as_uint(v[0][3]);
-        const unsigned b0 = __float_as_uint(v[1][0]), b1 = __float_as_uint(v[1][1]);
-        const unsigned b2 = __float_as_uint(v[1][2]), b3 = __float_as_uint(v[1][3]);
-        const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-        const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-        const auto r2 = __builtin_amdgcn_permlane32_swap(a2, b2, false, false);
-        const auto r3 = __builtin_amdgcn_permlane32_swap(a3, b3, false, false);
-        // lane now holds 8 consecutive channels: (r0[0], r1[0], r2[0], r3[0], r0[1], ..., r3[1])
-        const float f[8] = {__uint_as_float(r0[0]), __uint_as_float(r1[0]), __uint_as_float(r2[0]),
-                            __uint_as_float(r3[0]), __uint_as_float(r0[1]), __uint_as_float(r1[1]),
-                            __uint_as_float(r2[1]), __uint_as_float(r3[1])};
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][e]), __float_as_uint(v[1][e]), false,
+                                                          false);
+          f[e] = __uint_as_float(r[0]);
+          f[4 + e] = __uint_as_float(r[1]);
+        }
         unsigned o[4];
         if constexpr (MODE != 1) {
-          const uint4 sk = S.a[2 * i + m];
+          const uint4 sk = A.a[2 * i + m];
           const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -180,35 +191,73 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
             o[e] = pack2<T>(u0, u1);
           }
         }
-        if (tg >= 0) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
+        if (tg >= 0 && !(p.ablate & 1)) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
       }
   };
 
-  // one tile ahead, two register sets (loop unrolled by two so the sets stay in registers)
-  Set s0, s1;
-  load(t_begin, s0);
-  for (int t = t_begin; t < t_end; t += 2) {
-    if (t + 1 < t_end) load(t + 1, s1);
-    compute_store(t, s0);
-    if (t + 1 >= t_end) break;
-    if (t + 2 < t_end) load(t + 2, s0);
-    compute_store(t + 1, s1);
+  // Steps (tile, phase) in order; the operands of the next step are loaded before the current
+  // step's stores are issued (vector memory completes in issue order). Register sets
+  // alternate: x by tile parity, skip by step parity (NP is 1 or even) -> unrolled by 2 tiles.
+  XSet x0, x1;
+  ASet a0, a1;
+  load_x(t_begin, x0);
+  load_a(t_begin, 0, a0);
+  if constexpr (NP == 1) {
+    // single phase: both sets alternate per tile
+    for (int t = t_begin; t < t_end; t += 2) {
+      if (t + 1 < t_end) {
+        load_x(t + 1, x1);
+        load_a(t + 1, 0, a1);
+      }
+      compute_store(t, 0, x0, a0);
+      if (t + 1 >= t_end) break;
+      if (t + 2 < t_end) {
+        load_x(t + 2, x0);
+        load_a(t + 2, 0, a0);
+      }
+      compute_store(t + 1, 0, x1, a1);
+    }
+  } else {
+    // NP (even) phases per tile: skip sets alternate per phase (even phases a0), x per tile
+    auto tile = [&](int t, XSet& xc, XSet& xn) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ph = 0; ph < NP; ph += 2) {
+        load_a(t, ph + 1, a1);
+        compute_store(t, ph, xc, a0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ph + 2 < NP) {
+          load_a(t, ph + 2, a0);
+        } else if (t + 1 < t_end) {
+          load_x(t + 1, xn);
+          load_a(t + 1, 0, a0);
+        }
+        compute_store(t, ph + 1, xc, a1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    for (int t = t_begin; t < t_end; t += 2) {
+      tile(t, x0, x1);
+      if (t + 1 >= t_end) break;
+      tile(t + 1, x1, x0);
+    }
   }
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, int NP>
 static int launch_t(const ConvTParams& p, hipStream_t s) {
-  auto k = convt_add<T, MODE>;
+  auto k = convt_add<T, MODE, NP>;
+  constexpr int lds = lds_bytes<NP>();
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) {
       set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
       return 3;
     }
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3((MODE == 0 ? p.s * p.s : 1) * p.nchunks), dim3(NT), LDS, s, p);
+  const int groups = p.s * p.s / NP;
+  hipLaunchKernelGGL(k, dim3(groups * p.nchunks), dim3(NT), lds, s, p);
   TV_HIP(hipGetLastError());
   return 0;
 }
@@ -219,17 +268,21 @@ bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc) {
   return cin == convt::KJ * 16 && cout == convt::C && src_ldc % 8 == 0 && add_ldc % 8 == 0 && out_ldc % 8 == 0;
 }
 
-// tiles per wave: about 2 resident workgroups (8 waves) per CU over the whole launch, at least 4 tiles per wave
+// tiles per wave: about one resident 8-wave workgroup per CU over the whole launch, >= 2 tiles per wave
 void convt_schedule(ConvTParams& p, int cu_count) {
   if (p.mode != 0) p.s = 1;  // one "phase"
   const long M = (long)p.B * (p.mode != 0 ? (long)p.tH * p.tW : (long)p.h * p.w);
   const long mt = (M + 31) / 32;
-  const long waves_target = 2L * 4 * cu_count;  // 2 workgroups x 4 waves per CU
-  long per_phase = (waves_target + p.s * p.s - 1) / (p.s * p.s);
-  long tpw = (mt + per_phase - 1) / per_phase;
-  if (tpw < 4) tpw = 4;
+  const long waves_target = (long)convt::NW * cu_count;
+  // phase groups of 4 once every wave of the launch gets >= 2 tiles that way
+  p.np = (p.mode == 0 && p.s * p.s % convt::NPG == 0 &&
+          mt * (p.s * p.s / convt::NPG) >= 2 * waves_target) ? convt::NPG : 1;
+  const long groups = (long)p.s * p.s / p.np;
+  long per_group = (waves_target + groups - 1) / groups;
+  long tpw = (mt + per_group - 1) / per_group;
+  if (tpw < 1) tpw = 1;
   p.tpw = (int)tpw;
-  p.nchunks = (int)((mt + 4 * tpw - 1) / (4 * tpw));
+  p.nchunks = (int)((mt + convt::NW * tpw - 1) / (convt::NW * tpw));
 }
 
 int launch_convt(const ConvTParams& p, int dtype, hipStream_t s) {
@@ -238,14 +291,18 @@ int launch_convt(const ConvTParams& p, int dtype, hipStream_t s) {
     return 1;
   }
   using L = int (*)(const ConvTParams&, hipStream_t);
-  static const L f16[3] = {convt::launch_t<_Float16, 0>, convt::launch_t<_Float16, 1>, convt::launch_t<_Float16, 2>};
-  static const L b16[3] = {convt::launch_t<__bf16, 0>, convt::launch_t<__bf16, 1>, convt::launch_t<__bf16, 2>};
-  if (p.mode < 0 || p.mode > 2) {
+  using namespace convt;
+  static const L f16[4] = {launch_t<_Float16, 0, 1>, launch_t<_Float16, 1, 1>, launch_t<_Float16, 2, 1>,
+                           launch_t<_Float16, 0, NPG>};
+  static const L b16[4] = {launch_t<__bf16, 0, 1>, launch_t<__bf16, 1, 1>, launch_t<__bf16, 2, 1>,
+                           launch_t<__bf16, 0, NPG>};
+  if (p.mode < 0 || p.mode > 2 || (p.np != 1 && !(p.mode == 0 && p.np == NPG))) {
     set_error("convt: bad mode");
     return 1;
   }
-  if (dtype == F16) return f16[p.mode](p, s);
-  if (dtype == BF16) return b16[p.mode](p, s);
+  const int v = p.np == NPG ? 3 : p.mode;
+  if (dtype == F16) return f16[v](p, s);
+  if (dtype == BF16) return b16[v](p, s);
   set_error("convt: fp16/bf16 only");
   return 1;
 }

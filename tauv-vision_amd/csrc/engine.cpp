@@ -564,6 +564,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
     t.sy = op.sy;
     t.sx = op.sx;
     convt_schedule(t, cu_count);
+    if (const char* env = std::getenv("TV_CONVT_ABLATE")) t.ablate = std::atoi(env);
     ws->convt[i] = 1;
     ws->use_pipe[i] = 0;
   }

@@ -8,7 +8,7 @@ cd "$ROOT/tauv-vision_amd"
 name=$1; target=$2; src=$(realpath "$ROOT/$3"); shift 3
 mkdir -p build/var_$name lib/variants
 objs=""
-for f in csrc/conv.hip csrc/conv_pipe.hip csrc/conv_halo.hip csrc/conv3x3.hip csrc/aux.hip csrc/decode.hip csrc/planner.cpp csrc/engine.cpp csrc/capi.cpp; do
+for f in $(sed -n "s/^SRC := //p" Makefile); do
   b=$(basename $f)
   if [ "$b" = "$target" ]; then
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Icsrc "$@" -x hip -c "$src" -o build/var_$name/$b.o

@@ -21,9 +21,8 @@
 //    buffer-OOB, so they read as zero with no per-lane branches) and the 9 taps read shifted
 //    windows of it at compile-time immediate ds_read offsets: 1.2x input traffic instead of 9x;
 //  * two halo buffers (the next channel block — or the next tile's first — streams in during
-//    taps 0..5 of the current one), a 3-slot weight ring (8 KiB per k-step from a k-step-major,
-//    pre-swizzled copy of the weights: each wave's 1 KiB piece is contiguous; loaded into
-//    registers three k-steps ahead and written with ds_write_b128 one step later), one raw
+//    taps 0..5 of the current one), a 5-slot weight ring (8 KiB per k-step, LDS-DMA from a
+//    k-step-major, pre-swizzled copy of the weights: each 1 KiB piece is contiguous), one raw
 //    s_barrier per k-step with an exact counted vmcnt;
 //  * fragment reads run one 16-deep sub-step ahead of the MFMAs (6 ds_read_b128 per half
 //    k-step, two register sets) and the k-step's LDS-DMA pieces are issued between MFMA pairs;
@@ -31,7 +30,7 @@
 //    pack, v_permlane32_swap pairs into 16-byte stores), so the next tile's prefetched halo and
 //    weights are already in flight while it runs: no per-tile prologue, no LDS staging.
 // LDS: halo 2 x 48 KiB (pixel pitch 80 B = 64 B of channels + 16 B pad: conflict-free
-// ds_read_b128 for 32-pixel rows), weight ring 3 x 8 KiB (XOR-swizzled 64 B rows), bias.
+// ds_read_b128 for 32-pixel rows), weight ring 5 x 8 KiB (XOR-swizzled 64 B rows), bias.
 #include "conv_common.h"
 
 #include <type_traits>
@@ -51,6 +50,7 @@ constexpr int HBUF = HPIECES * 1024;          // one halo buffer
 constexpr int HPW = HPIECES / NW;             // halo pieces per wave per channel block = 6
 constexpr int HTAPS = HPW;                    // one halo piece per k-step, taps 0..5
 constexpr int WSLOT = BN * 64;                // weights of one k-step: 128 rows x 64 B
+constexpr int D = 4;                          // weight prefetch distance (k-steps)
 constexpr int RING = 3;                       // weight ring slots (register-staged: k-step q is
                                               // loaded at step q-3, written to LDS at step q-2)
 constexpr int OFF_W = 2 * HBUF;
@@ -343,7 +343,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     }
   };
 
-  // ---- prologue: halo of (tile 0, block 0), weights of k-steps 0..2
+  // ---- prologue: halo of (tile 0, block 0), weights of k-steps 0..D-1
   int cur_fr, cur_y0, cur_x0, cur_nt;
   tile_of(0, cur_fr, cur_y0, cur_x0, cur_nt);
   halo_offsets(cur_fr, cur_y0, cur_x0);

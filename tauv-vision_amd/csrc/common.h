@@ -103,6 +103,12 @@ constexpr int kConv3MaxN = 1024;
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
                    hipStream_t s, int epi = 0);
 int conv3x3_tiles(int B, int H, int W, int tw);
+// Persistent halo-tile 3x3 / stride 2 / pad 1 kernel (conv3x3s2.hip), fp16/bf16, 128 -> 128
+// channels: 16x32-pixel output tiles; ConvParams.mtiles = conv3x3s2_tiles(B, Ho, Wo), ntiles = 1
+int conv3x3s2_tiles(int B, int Ho, int Wo);
+size_t conv3x3s2_weight_bytes();
+int conv3x3s2_repack(const void* w, int Kpad, int esz, void* out, hipStream_t s);
+int launch_conv3x3s2(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int grid, hipStream_t s);
 // k-step-major, pre-swizzled weight copy the kernel streams (from the [Npad][Kpad] packing)
 size_t conv3x3_weight_bytes(int ntiles);
 int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, void* out, hipStream_t s);

@@ -224,7 +224,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   // ---- weight issue cursor: k-step counter and the global k-step index of the next piece
-  int wc_q = 0, wc_idx = 0, wc_in = 0, wc_nt = 0;
+  int wc_idx = 0, wc_in = 0, wc_nt = 0;
   {
     int a, b_, c_;
     tile_of(0, a, b_, c_, wc_nt);
@@ -235,7 +235,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto w_load = [&](u32x4& dst) __attribute__((always_inline)) {
     const char* src = wts + (size_t)(wc_nt * SPT + wc_in) * WSLOT;
     dst = *(g_cu32x4*)src;
-    ++wc_q;
     if (++wc_in == SPT) {
       wc_in = 0;
       if (++wc_idx < ntl) {

@@ -244,6 +244,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_SLICES")) slices = std::atoi(env);
   // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
@@ -389,6 +390,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->halo_tw.assign(plan.ops.size(), 0);
   ws->c3_tw.assign(plan.ops.size(), 0);
   ws->c3_grid.assign(plan.ops.size(), 0);
+  ws->s2_grid.assign(plan.ops.size(), 0);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (op.kind == OP_PREP) continue;
@@ -477,6 +479,33 @@ int Engine::make_workspace(int B, Workspace* ws) {
         ws->halo_tw[i] = 0;
         ws->use_pipe[i] = 0;
         p.mtiles = mt;
+      }
+    }
+    // persistent stride-2 3x3 kernel (conv3x3s2.hip): 128 -> 128 channels, fp16/bf16, at least
+    // one 512-pixel tile per CU (smaller layers stay on the pipelined implicit GEMM)
+    if (s2_mode && dtype != F32 && op.kind == OP_CONV && op.segs.size() == 1 && op.out >= 0 && op.add < 0) {
+      const SegSpec& sg = op.segs[0];
+      const ConvSegment& cs = p.seg[0];
+      const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
+      const size_t frame_bytes = (size_t)cs.H * cs.W * cs.ldc * esz;
+      const int mt = conv3x3s2_tiles(B, p.Ho, p.Wo);
+      if (sg.kh == 3 && sg.kw == 3 && sg.stride == 2 && sg.pad == 1 && pw == 1 && !sg.row_expand && cs.C == 128 &&
+          p.N == 128 && p.ntiles == 1 && cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && frame_bytes < (1ull << 31) &&
+          mt >= cu_count) {
+        Packed& pk3 = packed[i];
+        if (!pk3.w_c3) {
+          TV_HIP(hipMalloc(&pk3.w_c3, conv3x3s2_weight_bytes()));
+          int rc = conv3x3s2_repack(pk3.w, pk3.Kpad, esz, pk3.w_c3, nullptr);
+          if (rc) return rc;
+          TV_HIP(hipDeviceSynchronize());
+        }
+        int grid = std::min(mt, cu_count);
+        if (grid >= 8) grid -= grid % 8;
+        p.weight = pk3.w_c3;
+        p.mtiles = mt;
+        ws->s2_grid[i] = grid;
+        ws->use_pipe[i] = 0;
+        ws->halo_tw[i] = 0;
       }
     }
   }
@@ -655,7 +684,8 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
-  int rc = ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s)
+  int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
+           : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s)
            : ws->halo_tw[i] ? launch_conv_halo(p, ws->dparams + i, p.out, dtype, out_f32, ws->halo_tw[i], s)
            : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
                              : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
@@ -762,6 +792,7 @@ const char* Engine::op_kernel(int B, size_t i) {
     if (name.empty()) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].mode) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
+      else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ">";
       else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";

@@ -13,7 +13,7 @@ namespace tv {
 
 struct Packed {
   void* w = nullptr;       // [Npad][Kpad] compute dtype
-  void* w_c3 = nullptr;    // conv3x3.hip k-step-major copy (made on first use)
+  void* w_c3 = nullptr;    // conv3x3.hip / conv3x3s2.hip k-step-major copy (made on first use)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;
@@ -35,6 +35,7 @@ struct Workspace {
   std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
   std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
   std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
+  std::vector<int> s2_grid;         // per op: > 0 = persistent stride-2 conv3x3s2 (workgroups)
   std::vector<int> head_fused;      // per op: 1 = stacked 3x3 heads with the 1x1 heads fused in
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
@@ -53,6 +54,7 @@ struct Engine {
   size_t weight_bytes = 0;
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
   int pipe_mode = 1;           // -1 auto (>= 256 tiles), 0 never, 1 whenever representable (env TV_CONV_PIPE)
+  int s2_mode = 1;             // stride-2 halo kernel for eligible fp16/bf16 layers (env TV_CONV3S2=0 off)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
   int cu_count = 256;          // compute units (persistent grids)
   int headfuse_mode = 1;       // fuse the 1x1 heads into the 3x3 heads epilogue (env TV_HEADFUSE=0 off)

@@ -100,8 +100,10 @@ int halo_tiles(int B, int H, int W, int tw);
 // persistent workgroups (one per CU, a multiple of 8 when >= 8).
 constexpr int kConv3MaxN = 1024;
 // epi = 0: store the activations; epi = 1: fused 1x1 heads into the fp32 output `out` (head_*)
+// res = 1: two segments — seg 0 the 3x3 input, seg 1 a 1x1 conv (stride seg[1].stride) over a
+// 128-channel tensor summed into the same accumulators (ResidualBlock conv2 + conv_residual)
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s, int epi = 0);
+                   hipStream_t s, int epi = 0, int res = 0);
 int conv3x3_tiles(int B, int H, int W, int tw);
 // Persistent halo-tile 3x3 / stride 2 / pad 1 kernel (conv3x3s2.hip), fp16/bf16, 128 -> 128
 // channels: 16x32-pixel output tiles; ConvParams.mtiles = conv3x3s2_tiles(B, Ho, Wo), ntiles = 1
@@ -110,8 +112,8 @@ size_t conv3x3s2_weight_bytes();
 int conv3x3s2_repack(const void* w, int Kpad, int esz, void* out, hipStream_t s);
 int launch_conv3x3s2(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int grid, hipStream_t s);
 // k-step-major, pre-swizzled weight copy the kernel streams (from the [Npad][Kpad] packing)
-size_t conv3x3_weight_bytes(int ntiles);
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, void* out, hipStream_t s);
+size_t conv3x3_weight_bytes(int ntiles, int res);
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, void* out, hipStream_t s);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
@@ -145,9 +147,6 @@ struct ConvTParams {
   int out_ldc;
   int B, s, tH, tW, sy, sx;
   int tpw, nchunks, np;  // schedule (convt_schedule): tiles per wave, workgroups per phase group, phases per group
-  int mode;           // 0: ConvTranspose + add; 1: 1x1 conv, out (b,oy,ox) <- src (b,oy*stride,ox*stride);
-                      // 2: mode 1 + add[b,oy,ox] before the activation
-  int stride, act;    // modes 1, 2
   int ablate;         // timing experiments only (env TV_CONVT_ABLATE): 1 no stores, 2 no MFMA, 4 no skip loads
 };
 bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc);

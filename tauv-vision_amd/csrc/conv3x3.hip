@@ -43,7 +43,8 @@ constexpr int NT = 512, NW = 8, BN = 128, P = 512;
 constexpr int WP = P / NW;                    // pixels per wave = 64 (two 32-pixel fragments)
 constexpr int CBK = 32;                       // channels per k-step
 constexpr int NCB = 128 / CBK;                // channel blocks per tile (C == 128)
-constexpr int SPT = 9 * NCB;                  // k-steps per tile
+template <int RES>
+constexpr int spt() { return (9 + RES) * NCB; }
 constexpr int PITCH = 80;                     // halo pixel pitch (bytes)
 constexpr int HPIX = 612;                     // (16+2)x(32+2) = (32+2)x(16+2) halo pixels
 constexpr int HPIECES = 48;                   // ceil(612 * 5 / 64) LDS-DMA pieces of 1 KiB
@@ -55,7 +56,12 @@ constexpr int RING = 3;                       // weight ring slots (register-sta
                                               // loaded at step q-3, written to LDS at step q-2)
 constexpr int OFF_W = 2 * HBUF;
 constexpr int OFF_B = OFF_W + RING * WSLOT;
-constexpr int LDS = OFF_B + kConv3MaxN * 4;
+constexpr int OFF_R = OFF_B + kConv3MaxN * 4;  // RES: one channel block of the residual input
+constexpr int RBUF = 512 * 64;                  // 512 pixels x 32 channels (XOR-swizzled 16 B chunks)
+constexpr int RPW = RBUF / 1024 / NW;           // residual pieces per wave per channel block = 4
+template <int RES>
+constexpr int lds_bytes() { return OFF_R + (RES ? RBUF : 0); }
+static_assert(lds_bytes<1>() <= 160 * 1024, "LDS budget");
 static_assert(WSLOT / 1024 == NW, "one weight piece per wave per k-step");
 static_assert(HPIECES * 64 >= HPIX * 5, "halo pieces");
 
@@ -119,9 +125,10 @@ __device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh
   gstore16(dst + 8 * lh, make_uint4(r0[0], r1[0], r0[1], r1[1]));
 }
 
-template <typename T, typename OutT, int TW, int ACT, int EPI>
+template <typename T, typename OutT, int TW, int ACT, int EPI, int RES>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
+  constexpr int SPTK = spt<RES>();  // k-steps per tile
   constexpr int TH = P / TW;
   constexpr int RS = TW + 2;                               // halo row stride (pixels)
   constexpr int FOFF = (TW == 32 ? 1 : 2) * RS * PITCH;    // next 32-pixel fragment
@@ -161,7 +168,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
   if (ntl == 0) return;
-  const int S_tot = ntl * SPT;
+  const int S_tot = ntl * SPTK;
 
   // bias of every output channel into LDS (read in the epilogues)
   float* lbias = reinterpret_cast<float*>(smem + OFF_B);
@@ -223,6 +230,40 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
                         cb * CBK * (int)sizeof(T), 0, 0);
   };
 
+  // ---- RES: the ResidualBlock's 1x1 conv_residual (dla.py:32-37) as a 10th k-step per
+  // channel block. Its input x (second segment, stride rstr) for the tile's 512 output pixels
+  // moves into one 32 KiB LDS buffer per channel block: chunk L = piece*64 + lane holds pixel
+  // q = L/4, source chunk (L % 4) ^ ((q >> 2) & 3) (conflict-free fragment reads). One buffer
+  // resource per frame keeps offsets below 2^31.
+  [[maybe_unused]] unsigned rgeo[RPW];
+  [[maybe_unused]] const ConvSegment& sr = p.seg[RES ? 1 : 0];
+  [[maybe_unused]] const unsigned rpix_bytes = (unsigned)sr.ldc * (unsigned)sizeof(T);
+  if constexpr (RES) {
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int L = (wave * RPW + i) * 64 + lane;
+      const int q = L >> 2;
+      rgeo[i] = (unsigned)((q << 2) | ((L & 3) ^ ((q >> 2) & 3)));
+    }
+  }
+  auto res_piece = [&](int i, int fr, int y0, int x0, int cb) __attribute__((always_inline)) {
+    const unsigned long long fb = (unsigned long long)sr.H * sr.W * rpix_bytes;
+    const unsigned long long a = (unsigned long long)sr.src + (unsigned long long)fr * fb;
+    i32x4 rs;
+    rs.x = (int)(unsigned)a;
+    rs.y = (int)(unsigned)(a >> 32);
+    rs.z = (int)(unsigned)fb;
+    rs.w = 0x00020000;
+    const int q = (int)(rgeo[i] >> 2), c = (int)(rgeo[i] & 3);
+    const int y = y0 + q / TW, x = x0 + q % TW;
+    const bool ok = y < H && x < W;
+    const unsigned off = ok ? ((unsigned)(y * sr.stride) * (unsigned)sr.W + (unsigned)(x * sr.stride)) * rpix_bytes +
+                                  (unsigned)c * 16u
+                            : 0x80000000u;
+    raw_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + OFF_R + (wave * RPW + i) * 1024), 16,
+                        (int)off, cb * CBK * (int)sizeof(T), 0, 0);
+  };
+
   // ---- weight issue cursor: k-step counter and the global k-step index of the next piece
   int wc_idx = 0, wc_in = 0, wc_nt = 0;
   {
@@ -233,9 +274,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // ring slot with ds_write_b128 one step later (instead of an LDS-DMA piece per k-step)
   u32x4 wreg[2];
   auto w_load = [&](u32x4& dst) __attribute__((always_inline)) {
-    const char* src = wts + (size_t)(wc_nt * SPT + wc_in) * WSLOT;
+    const char* src = wts + (size_t)(wc_nt * SPTK + wc_in) * WSLOT;
     dst = *(g_cu32x4*)src;
-    if (++wc_in == SPT) {
+    if (++wc_in == SPTK) {
       wc_in = 0;
       if (++wc_idx < ntl) {
         int a, b_, c_;
@@ -257,12 +298,26 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   for (int j = 0; j < 2; ++j)
     wa[j] = lds0 + OFF_W + (unsigned)(l32 * 64 + (((2 * j + lh) ^ ((l32 >> 2) & 3)) << 4));
 
-  // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]
+  // RES: fragment base of pixel q0 = WP*wave + l32 in the residual buffer, per sub-step J
+  // (fragment f = 1 is q0 + 32: +2 KiB, same swizzle)
+  [[maybe_unused]] unsigned rxa[2];
+  if constexpr (RES) {
+    const int q0 = WP * wave + l32;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) rxa[j] = lds0 + OFF_R + (unsigned)(q0 * 64 + (((2 * j + lh) ^ ((q0 >> 2) & 3)) << 4));
+  }
+
+  // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]; TAP 9 = residual k-step
   auto read_one = [&](auto r, auto j, auto tap, unsigned xb, unsigned wb, Half& F) __attribute__((always_inline)) {
     constexpr int R = decltype(r)::value, J = decltype(j)::value, TAP = decltype(tap)::value;
-    constexpr int TOFF = ((TAP / 3) * RS + (TAP % 3)) * PITCH;
-    if constexpr (R < 2) F.x[R] = ds_read16<TOFF + 32 * J + R * FOFF>(xb);
-    else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
+    if constexpr (TAP == 9) {
+      if constexpr (R < 2) F.x[R] = ds_read16<R * 2048>(rxa[J]);
+      else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
+    } else {
+      constexpr int TOFF = ((TAP / 3) * RS + (TAP % 3)) * PITCH;
+      if constexpr (R < 2) F.x[R] = ds_read16<TOFF + 32 * J + R * FOFF>(xb);
+      else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
+    }
   };
 
   f32x16 acc[2][4];  // [pixel fragment f][channel fragment i]; first written by a tile's first k-step
@@ -385,34 +440,37 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // Halo buffer of channel block cb is cb & 1 (NCB is even, so parity is per-tile fixed).
   auto step = [&](auto tap, auto first, auto par) __attribute__((always_inline)) {
     constexpr int TAP = decltype(tap)::value;
-    // LDS-DMA instructions allowed in flight: those issued after weights(s+1) — weight pieces
-    // of s+2, s+3 (issued at steps s-2, s-1) and halo pieces at steps s-3..s-1 of this channel
-    // block with tap < HTAPS — except at tap 8, where the next k-step reads the NEXT channel
-    // block's halo: then every halo piece must have landed (only the 2 weight pieces issued
-    // after the last one, at taps 6 and 7, may stay in flight)
-    // Weights of k-step s+1 were written to LDS at step s-1 (lgkmcnt + barrier below). At tap
-    // 8 the next k-step reads the NEXT channel block's halo (pieces issued at taps 0..5): every
-    // halo piece must have landed; only the weight loads issued after the last one (at taps 6
-    // and 7, for k-steps s+1 and s+2... i.e. issued while s+1, s+2 < S_tot) may stay in flight.
+    // Weights of k-step s+1 were written to LDS at step s-1 (lgkmcnt + barrier below); halo and
+    // residual data arrive by LDS-DMA and are waited for with an exact vmcnt: the count of
+    // vector-memory operations issued after the last piece the next k-step reads. A weight load
+    // was issued at step q iff q + 3 < S_tot; within a step the order is weight load, halo piece
+    // (taps 0..5, next channel block), residual piece (RES, taps 1..4, this channel block).
+    //  * tap 8 without RES / residual step (tap 9): the next k-step reads the NEXT channel
+    //    block's halo (last piece at tap 5): younger = the weight loads of taps 6, 7 (and 8);
+    //  * tap 8 with RES: the residual step reads this block's residual input (last piece at
+    //    tap 4): younger = weight loads of taps 5, 6, 7 + the tap-5 halo piece.
     static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
+    auto wl = [&](int q) { return q >= 0 && q + 3 < S_tot ? 1 : 0; };
     unsigned long long tw0 = 0;
     if (p.stamps) tw0 = __builtin_amdgcn_s_memtime();
-    if constexpr (TAP == 8) wait_vm_n(s + 1 < S_tot ? (s + 1 < S_tot) + (s + 2 < S_tot) : 0);
+    if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 2) + wl(s - 1) : 0);
+    if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) + (nxt_exists ? 1 : 0) : 0);
+    if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (p.stamps) stall += __builtin_amdgcn_s_memtime() - tw0;
 
-    constexpr int NTAP = TAP == 8 ? 0 : TAP + 1;
+    constexpr int NTAP = TAP == 8 ? (RES ? 9 : 0) : TAP == 9 ? 0 : TAP + 1;
     const bool do_r = s + 1 < S_tot;
     const int hbuf = (cb + 1) & 1;
-    const unsigned xc = xa + (cb & 1) * HBUF;                         // this k-step's halo
-    const unsigned xn = xa + (TAP == 8 ? hbuf : (cb & 1)) * HBUF;     // next k-step's halo
+    const unsigned xc = xa + (cb & 1) * HBUF;                                  // this k-step's halo
+    const unsigned xn = xa + (NTAP == 0 ? hbuf : (cb & 1)) * HBUF;             // next k-step's halo
     const unsigned wc1 = wa[1] + (unsigned)((s % RING) * WSLOT);
     const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
-    constexpr int PAR = decltype(par)::value;  // parity of s (36 k-steps per tile: static)
+    constexpr int PAR = decltype(par)::value;  // parity of s (36 or 40 k-steps per tile: static)
     if (s + 3 < S_tot) w_load(wreg[PAR ^ 1]);   // k-step s+3 (that set's k-step s+1 is in LDS)
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
@@ -438,6 +496,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     if constexpr (TAP < HTAPS)
       if (nxt_exists) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);
+    if constexpr (RES && TAP >= 1 && TAP <= RPW) res_piece(TAP - 1, cur_fr, cur_y0, cur_x0, cb);
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<3>{}, IC<FIRST>{}, H0);
     __builtin_amdgcn_sched_barrier(0);
@@ -471,7 +530,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     cb = CB;
     nxt_newtile = CB + 1 == NCB;
     nxt_exists = !nxt_newtile || tl + 1 < ntl;
-    constexpr int P0 = (CB * 9) & 1;
+    constexpr int P0 = (CB * (9 + RES)) & 1;
     step(IC<0>{}, IC<CB == 0>{}, IC<P0>{});
     step(IC<1>{}, IC<false>{}, IC<P0 ^ 1>{});
     step(IC<2>{}, IC<false>{}, IC<P0>{});
@@ -481,6 +540,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     step(IC<6>{}, IC<false>{}, IC<P0>{});
     step(IC<7>{}, IC<false>{}, IC<P0 ^ 1>{});
     step(IC<8>{}, IC<false>{}, IC<P0>{});
+    if constexpr (RES) step(IC<9>{}, IC<false>{}, IC<P0 ^ 1>{});
   };
 
   // 4 channel blocks per tile, fully unrolled (36 k-steps of straight-line code): the
@@ -508,32 +568,35 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 }
 
-// [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q = cb*9 + tap][128 rows][4 x 16 B],
-// slot s of row r holding chunk s ^ ((r >> 2) & 3) of the k-step
-__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, uint4* __restrict__ out) {
-  const int n = ntiles * SPT * BN * 4;
+// [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q][128 rows][4 x 16 B], q = cb*9 + tap
+// (res: q = cb*10 + j, j = 9 the residual segment's channel block cb at K offset 9*128), slot s
+// of row r holding chunk s ^ ((r >> 2) & 3) of the k-step
+__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, int res, uint4* __restrict__ out) {
+  const int sp = res ? spt<1>() : spt<0>();
+  const int n = ntiles * sp * BN * 4;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
-    const int slot = o & 3, row = (o >> 2) & (BN - 1), q = (o >> 9) % SPT, nt = (o >> 9) / SPT;
+    const int slot = o & 3, row = (o >> 2) & (BN - 1), q = (o >> 9) % sp, nt = (o >> 9) / sp;
     const int chunk = slot ^ ((row >> 2) & 3);
-    const int cb = q / 9, tap = q - cb * 9;
-    const int k16 = (tap * 128 + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements)
+    const int cb = q / (9 + res), tap = q - cb * (9 + res);
+    const int k16 = (tap * 128 + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements); tap 9 = residual
     out[o] = w[(size_t)(nt * BN + row) * kpad16 + k16];
   }
 }
 
-template <typename T, int TW, int ACT, int EPI = 0>
+template <typename T, int TW, int ACT, int EPI = 0, int RES = 0>
 static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
-  auto k = conv3x3<T, T, TW, ACT, EPI>;
+  auto k = conv3x3<T, T, TW, ACT, EPI, RES>;
+  constexpr int lds = lds_bytes<RES>();
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) {
       set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
       return 3;
     }
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), LDS, s, dp, out);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, out);
   TV_HIP(hipGetLastError());
   return 0;
 }
@@ -545,24 +608,36 @@ int conv3x3_tiles(int B, int H, int W, int tw) {
   return B * ((H + th - 1) / th) * ((W + tw - 1) / tw);
 }
 
-size_t conv3x3_weight_bytes(int ntiles) { return (size_t)ntiles * c3::SPT * c3::WSLOT; }
+size_t conv3x3_weight_bytes(int ntiles, int res) {
+  return (size_t)ntiles * (res ? c3::spt<1>() : c3::spt<0>()) * c3::WSLOT;
+}
 
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, void* out, hipStream_t s) {
-  if ((Kpad * esz) % 16 || Kpad < 9 * 128) {
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, void* out, hipStream_t s) {
+  if ((Kpad * esz) % 16 || Kpad < (res ? 10 : 9) * 128) {
     set_error("conv3x3_repack: bad Kpad");
     return 1;
   }
-  hipLaunchKernelGGL(c3::repack_weights, dim3(256), dim3(256), 0, s, (const uint4*)w, Kpad * esz / 16, ntiles,
+  hipLaunchKernelGGL(c3::repack_weights, dim3(256), dim3(256), 0, s, (const uint4*)w, Kpad * esz / 16, ntiles, res,
                      (uint4*)out);
   TV_HIP(hipGetLastError());
   return 0;
 }
 
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s, int epi) {
+                   hipStream_t s, int epi, int res) {
   using namespace c3;
   if (p.act < 0 || p.act > 2) {
     set_error("conv3x3: bad activation");
+    return 1;
+  }
+  if (res) {  // ResidualBlock conv2 + conv_residual: ReLU, plain stores
+    if (p.act != 1 || epi != 0 || p.nseg != 2 || p.ntiles != 1) {
+      set_error("conv3x3: residual k-steps need ReLU, one channel tile and two segments");
+      return 1;
+    }
+    if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 1, 0, 1>(p, dp, out, grid, s) : launch_t<_Float16, 16, 1, 0, 1>(p, dp, out, grid, s);
+    if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 1, 0, 1>(p, dp, out, grid, s) : launch_t<__bf16, 16, 1, 0, 1>(p, dp, out, grid, s);
+    set_error("conv3x3: fp16/bf16 only");
     return 1;
   }
   if (epi == 1) {  // fused 1x1 heads: the stacked heads' LeakyReLU only

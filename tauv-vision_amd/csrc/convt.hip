@@ -18,12 +18,6 @@
 //  * the epilogue works on the accumulators in place (bias, + skip in fp32, one rounding,
 //    v_permlane32_swap into 16-byte stores), in the same arithmetic order as conv_pipe's
 //    mode-1 epilogue: (acc + bias) + skip.
-//
-// MODE 1 reuses the same machinery for a 1x1 convolution with stride: output pixel (b, oy, ox)
-// reads input pixel (b, oy*stride, ox*stride); optional ReLU. MODE 2 is MODE 1 plus a tensor
-// added at the output pixel before the ReLU: ResidualBlock's tail relu(bn2(conv2(y)) +
-// bn_residual(conv_residual(x))) (dla.py:39-52) when the planner splits the 1x1 residual out of
-// conv2's GEMM (conv2 then runs on the 3x3 halo kernel and stores bn2(conv2(y)) unactivated).
 #include "conv_common.h"
 
 namespace tv {
@@ -35,7 +29,7 @@ constexpr int C = 128;         // output channels per phase (4 MFMA row tiles)
 constexpr int KJ = 8;          // K = 128 input channels = 8 MFMA k-steps of 16
 constexpr int WPITCH = 272;    // LDS weight row pitch (bytes): odd multiple of 16 -> no bank conflicts
 constexpr int PW = C * WPITCH; // one phase's weights
-constexpr int NPG = 4;         // phases per workgroup (MODE 0): the input tile is loaded once for all
+constexpr int NPG = 4;         // phases per workgroup on large inputs: the input tile is loaded once for all
 template <int NP>
 constexpr int lds_bytes() { return NP * (PW + C * 4); }
 
@@ -60,14 +54,14 @@ struct ASet {
   uint4 a[8];    // skip / residual chunks (i, m): channels 32i + 16m + 8*lh .. +8 at the target pixel
 };
 
-// MODE 0: a workgroup owns NP consecutive phases of the s*s and a run of 32-pixel input tiles;
-// per tile a wave loads the input operand once and runs the NP phases, the skip chunks of the
-// next phase step in flight under the current one (NP = 4 on large inputs; NP = 1 spreads
-// small inputs over s*s times more workgroups). MODES 1, 2: NP = 1.
-template <typename T, int MODE, int NP>
+// A workgroup owns NP consecutive phases of the s*s and a run of 32-pixel input tiles; per tile
+// a wave loads the input operand once and runs the NP phases, the skip chunks of the next phase
+// step in flight under the current one (NP = 4 on large inputs; NP = 1 spreads small inputs over
+// s*s times more workgroups).
+template <typename T, int NP>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void convt_add(ConvTParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  static_assert(NP == 1 || (MODE == 0 && NP % 2 == 0), "phase group");
+  static_assert(NP == 1 || NP % 2 == 0, "phase group");
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -89,8 +83,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   __syncthreads();
 
-  // MODE 0: GEMM rows are input pixels (b, iy, ix); MODES 1, 2: output pixels (b, oy, ox)
-  const int hw = MODE == 0 ? p.h * p.w : p.tH * p.tW;
+  // GEMM rows are input pixels (b, iy, ix)
+  const int hw = p.h * p.w;
   const int M = p.B * hw;
   const int mt = (M + 31) / 32;
   const int t_begin = (chunk * NW + wave) * p.tpw;
@@ -101,7 +95,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto target = [&](int t, int ph) __attribute__((always_inline)) -> long long {
     const int m = t * 32 + l32;
     if (m >= M) return -1;
-    if constexpr (MODE != 0) return m;
     const int phase = phase0 + ph;
     const int py = phase / p.s, px = phase - py * p.s;
     const int b = m / hw;
@@ -113,20 +106,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
   auto load_x = [&](int t, XSet& S) __attribute__((always_inline)) {
     const int m = t * 32 + l32;
-    size_t sp = (size_t)(m < M ? m : 0);
-    if constexpr (MODE != 0) {  // strided 1x1: input pixel (b, oy*stride, ox*stride)
-      const int b = (int)sp / hw;
-      const int rem = (int)sp - b * hw;
-      const int oy = rem / p.tW, ox = rem - oy * p.tW;
-      sp = ((size_t)(b * p.h + oy * p.stride)) * p.w + (size_t)ox * p.stride;
-    }
+    const size_t sp = (size_t)(m < M ? m : 0);
     const T* src = reinterpret_cast<const T*>(p.src) + sp * p.src_ldc + 8 * lh;
 #pragma unroll
     for (int j = 0; j < KJ; ++j) S.x[j] = gload16(src + 16 * j);
   };
   auto load_a = [&](int t, int ph, ASet& S) __attribute__((always_inline)) {
-    if (MODE == 1 || (p.ablate & 4)) return;
-    const long long tg = target(t, ph);  // MODE 2: the output pixel itself
+    if (p.ablate & 4) return;
+    const long long tg = target(t, ph);
     const T* add = reinterpret_cast<const T*>(p.add) + (tg < 0 ? 0 : tg) * p.add_ldc + 8 * lh;
 #pragma unroll
     for (int q = 0; q < 8; ++q) S.a[q] = gload16(add + 16 * q);  // q = 2i + m -> channel 16q + 8lh
@@ -174,23 +161,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
           f[4 + e] = __uint_as_float(r[1]);
         }
         unsigned o[4];
-        if constexpr (MODE != 1) {
-          const uint4 sk = A.a[2 * i + m];
-          const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
+        const uint4 sk = A.a[2 * i + m];
+        const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float u0 = lo_f<T>(sw[e]) + f[2 * e], u1 = hi_f<T>(sw[e]) + f[2 * e + 1];
-            if (MODE == 2 && p.act == 1) u0 = fmaxf(u0, 0.0f), u1 = fmaxf(u1, 0.0f);
-            o[e] = pack2<T>(u0, u1);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float u0 = f[2 * e], u1 = f[2 * e + 1];
-            if (p.act == 1) u0 = fmaxf(u0, 0.0f), u1 = fmaxf(u1, 0.0f);
-            o[e] = pack2<T>(u0, u1);
-          }
-        }
+        for (int e = 0; e < 4; ++e) o[e] = pack2<T>(lo_f<T>(sw[e]) + f[2 * e], hi_f<T>(sw[e]) + f[2 * e + 1]);
         if (tg >= 0 && !(p.ablate & 1)) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
       }
   };
@@ -243,9 +217,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 }
 
-template <typename T, int MODE, int NP>
+template <typename T, int NP>
 static int launch_t(const ConvTParams& p, hipStream_t s) {
-  auto k = convt_add<T, MODE, NP>;
+  auto k = convt_add<T, NP>;
   constexpr int lds = lds_bytes<NP>();
   static bool attr = false;
   if (!attr) {
@@ -270,12 +244,11 @@ bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc) {
 
 // tiles per wave: about one resident 8-wave workgroup per CU over the whole launch, >= 2 tiles per wave
 void convt_schedule(ConvTParams& p, int cu_count) {
-  if (p.mode != 0) p.s = 1;  // one "phase"
-  const long M = (long)p.B * (p.mode != 0 ? (long)p.tH * p.tW : (long)p.h * p.w);
+  const long M = (long)p.B * p.h * p.w;
   const long mt = (M + 31) / 32;
   const long waves_target = (long)convt::NW * cu_count;
   // phase groups of 4 once every wave of the launch gets >= 2 tiles that way
-  p.np = (p.mode == 0 && p.s * p.s % convt::NPG == 0 &&
+  p.np = (p.s * p.s % convt::NPG == 0 &&
           mt * (p.s * p.s / convt::NPG) >= 2 * waves_target) ? convt::NPG : 1;
   const long groups = (long)p.s * p.s / p.np;
   long per_group = (waves_target + groups - 1) / groups;
@@ -290,19 +263,13 @@ int launch_convt(const ConvTParams& p, int dtype, hipStream_t s) {
     set_error("convt: not scheduled");
     return 1;
   }
-  using L = int (*)(const ConvTParams&, hipStream_t);
   using namespace convt;
-  static const L f16[4] = {launch_t<_Float16, 0, 1>, launch_t<_Float16, 1, 1>, launch_t<_Float16, 2, 1>,
-                           launch_t<_Float16, 0, NPG>};
-  static const L b16[4] = {launch_t<__bf16, 0, 1>, launch_t<__bf16, 1, 1>, launch_t<__bf16, 2, 1>,
-                           launch_t<__bf16, 0, NPG>};
-  if (p.mode < 0 || p.mode > 2 || (p.np != 1 && !(p.mode == 0 && p.np == NPG))) {
-    set_error("convt: bad mode");
+  if (p.np != 1 && p.np != NPG) {
+    set_error("convt: bad phase group");
     return 1;
   }
-  const int v = p.np == NPG ? 3 : p.mode;
-  if (dtype == F16) return f16[v](p, s);
-  if (dtype == BF16) return b16[v](p, s);
+  if (dtype == F16) return p.np == NPG ? launch_t<_Float16, NPG>(p, s) : launch_t<_Float16, 1>(p, s);
+  if (dtype == BF16) return p.np == NPG ? launch_t<__bf16, NPG>(p, s) : launch_t<__bf16, 1>(p, s);
   set_error("convt: fp16/bf16 only");
   return 1;
 }

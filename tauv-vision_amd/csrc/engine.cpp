@@ -391,6 +391,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->c3_tw.assign(plan.ops.size(), 0);
   ws->c3_grid.assign(plan.ops.size(), 0);
   ws->s2_grid.assign(plan.ops.size(), 0);
+  ws->c3_res.assign(plan.ops.size(), 0);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (op.kind == OP_PREP) continue;
@@ -452,7 +453,14 @@ int Engine::make_workspace(int B, Workspace* ws) {
     }
     // persistent halo-tile 3x3 kernel (conv3x3.hip): 3x3 / stride 1 / pad 1, one input of 128
     // channels, fp16/bf16, 16-byte aligned channel slices, byte offsets within 2^31
-    if (conv3_mode && dtype != F32 && op.kind == OP_CONV && op.segs.size() == 1 && op.out >= 0) {
+    // A second segment is accepted when it is ResidualBlock's 1x1 conv_residual (128 channels,
+    // stride 1 or 2, ReLU after the sum): one extra k-step per channel block (RES).
+    const bool res2 = op.segs.size() == 2 && op.segs[1].kh == 1 && op.segs[1].kw == 1 && op.segs[1].pad == 0 &&
+                      p.seg[1].C == 128 && p.seg[1].ldc % 8 == 0 && p.N == 128 && p.ntiles == 1 && op.act == 1 &&
+                      (size_t)p.seg[1].H * p.seg[1].W * p.seg[1].ldc * esz < (1ull << 31) &&
+                      p.seg[1].H >= (p.Ho - 1) * p.seg[1].stride + 1 && p.seg[1].W >= (p.Wo - 1) * p.seg[1].stride + 1;
+    if (conv3_mode && dtype != F32 && op.kind == OP_CONV && (op.segs.size() == 1 || res2) && op.out >= 0 &&
+        op.add < 0) {
       const SegSpec& sg = op.segs[0];
       const ConvSegment& cs = p.seg[0];
       const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
@@ -460,6 +468,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand && cs.C == 128 &&
           cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && src_bytes < (1ull << 31) &&
           p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2) {
+        const int res = res2 ? 1 : 0;
         const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16), t32 = conv3x3_tiles(B, cs.H, cs.W, 32);
         const int tw = t32 <= t16 ? 32 : 16;
         const int mt = tw == 32 ? t32 : t16;
@@ -468,13 +477,14 @@ int Engine::make_workspace(int B, Workspace* ws) {
         if (grid >= 8) grid -= grid % 8;
         Packed& pk3 = packed[i];
         if (!pk3.w_c3) {
-          TV_HIP(hipMalloc(&pk3.w_c3, conv3x3_weight_bytes(p.ntiles)));
-          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, pk3.w_c3, nullptr);
+          TV_HIP(hipMalloc(&pk3.w_c3, conv3x3_weight_bytes(p.ntiles, res)));
+          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, pk3.w_c3, nullptr);
           if (rc) return rc;
           TV_HIP(hipDeviceSynchronize());
         }
         p.weight = pk3.w_c3;
         ws->c3_tw[i] = tw;
+        ws->c3_res[i] = res;
         ws->c3_grid[i] = grid;
         ws->halo_tw[i] = 0;
         ws->use_pipe[i] = 0;
@@ -534,41 +544,6 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->tparams.assign(plan.ops.size(), ConvTParams{});
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
-    if (op.kind == OP_CONV && op.add >= 0) {
-      // split ResidualBlock tail: residual 1x1 GEMM + add + ReLU (convt.hip mode 2)
-      const SegSpec& sg = op.segs[0];
-      const TensorSpec& src = plan.tensors[sg.src];
-      const TensorSpec& tgt = plan.tensors[op.out];
-      const TensorSpec& add = plan.tensors[op.add];
-      if (dtype == F32 || op.segs.size() != 1 || sg.kh != 1 || sg.kw != 1 || sg.pad != 0 ||
-          !convt_supported(src.C, op.N, src.C, add.C, tgt.C)) {
-        set_error("residual tail " + op.label + ": no kernel for this shape");
-        return TV_ESHAPE;
-      }
-      ConvTParams& t = ws->tparams[i];
-      t.mode = 2;
-      t.src = base + ws->off[sg.src];
-      t.h = src.H;
-      t.w = src.W;
-      t.src_ldc = src.C;
-      t.stride = sg.stride;
-      t.act = op.act;
-      t.weight = packed[i].w;
-      t.Kpad = packed[i].Kpad;
-      t.bias = packed[i].bias;
-      t.add = base + ws->off[op.add];
-      t.add_ldc = add.C;
-      t.out = base + ws->off[op.out];
-      t.out_ldc = tgt.C;
-      t.B = B;
-      t.tH = tgt.H;
-      t.tW = tgt.W;
-      convt_schedule(t, cu_count);
-      ws->convt[i] = 1;
-      ws->use_pipe[i] = 0;
-      ws->c3_tw[i] = 0;
-      continue;
-    }
     if (!convt_mode || dtype == F32 || op.kind != OP_CONVT_ADD) continue;
     const TensorSpec& src = plan.tensors[op.src];
     const TensorSpec& tgt = plan.tensors[op.out];
@@ -672,7 +647,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   }
   if (ws->convt[i]) {
     int rc = launch_convt(ws->tparams[i], dtype, s);
-    if (rc || op.kind != OP_CONVT_ADD) return rc;
+    if (rc) return rc;
     const TensorSpec& tgt = plan.tensors[op.out];
     const ConvTParams& t = ws->tparams[i];
     if (op.cov_y0 > 0 || op.cov_x0 > 0 || op.cov_y1 < tgt.H || op.cov_x1 < tgt.W)
@@ -685,7 +660,8 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
-           : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s)
+           : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
+                                           ws->c3_res[i])
            : ws->halo_tw[i] ? launch_conv_halo(p, ws->dparams + i, p.out, dtype, out_f32, ws->halo_tw[i], s)
            : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
                              : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
@@ -790,10 +766,10 @@ const char* Engine::op_kernel(int B, size_t i) {
     const char* o = (op.out < 0) ? "float" : t;
     std::string& name = ws->kname[i];
     if (name.empty()) {
-      if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].mode) + ">";
+      if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
-      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ">";
+      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ">";
       else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";

@@ -35,6 +35,7 @@ struct Workspace {
   std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
   std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
   std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
+  std::vector<int> c3_res;          // per op: 1 = conv3x3 with the 1x1 residual segment (RES)
   std::vector<int> s2_grid;         // per op: > 0 = persistent stride-2 conv3x3s2 (workgroups)
   std::vector<int> head_fused;      // per op: 1 = stacked 3x3 heads with the 1x1 heads fused in
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before

@@ -19,9 +19,6 @@
 namespace tv {
 namespace {
 
-// ResidualBlocks whose output has at least this many pixels per frame are lowered as
-// conv2 (3x3 halo kernel) + residual GEMM with the add fused (fp16/bf16, 128 channels)
-constexpr int kSplitResidualPixels = 60 * 80;
 
 struct Walker {
   const tv_model_desc& d;
@@ -140,24 +137,6 @@ struct Walker {
   }
   int block(const std::string& p, int x, int cin, int cout, int stride) {
     int t = conv_bn_relu(p + ".conv1", p + ".bn1", x, cin, cout, 3, stride, 1);
-    const TensorSpec tt = P.tensors[t];
-    if (d.compute_dtype != F32 && cin == 128 && cout == 128 && tt.H * tt.W >= kSplitResidualPixels) {
-      // large 128-channel blocks in fp16/bf16: conv2 alone on the 3x3 halo kernel (bn2 folded,
-      // not activated), then the residual 1x1 GEMM with the tail add + ReLU fused (convt.hip
-      // mode 2): relu(bn2(conv2(t)) + bn_residual(conv_residual(x))) (dla.py:39-52)
-      int y2 = conv(p + ".conv2", {seg(t, p + ".conv2", p + ".bn2", 0, cout, 3, 1, 1)}, cout, 0);
-      OpSpec op;
-      op.kind = OP_CONV;
-      op.label = p + ".conv_residual+add+relu";
-      op.N = cout;
-      op.act = 1;
-      op.segs = {seg(x, p + ".conv_residual", p + ".bn_residual", 0, cin, 1, stride, 0)};
-      op.add = y2;
-      op.flops = 2.0 * tt.H * tt.W * (double)cout * cin;
-      op.out = tensor(tt.H, tt.W, cout);
-      P.ops.push_back(op);
-      return op.out;
-    }
     return conv(p + ".conv2+conv_residual",
                 {seg(t, p + ".conv2", p + ".bn2", 0, cout, 3, 1, 1),
                  seg(x, p + ".conv_residual", p + ".bn_residual", 0, cin, 1, stride, 0)},

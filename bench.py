@@ -88,13 +88,18 @@ def load_traffic(kernel, batch, precision):
 
 def conv_roofline(pipe, frames, precision, reps=3):
     """Per-launch HIP-event timing of one forward (tv_engine_profile: events recorded on the
-    launch stream around every launch; a separate pass after the timed region). The dominant
-    kernel is the conv instance with the largest summed time; achieved = its algorithmic FLOPs
-    (2*MAC per launch) / its summed launch durations (= FLOPs per launch / average
-    launch duration)."""
+    launch stream around every launch; a separate pass after the timed region). The timed path
+    launches a B-frame forward as concurrent slices (engine.slices), so the pass times one
+    slice's launches — the same kernel instances, grids and per-launch work rocprofv3 reports.
+    The dominant kernel is the conv instance with the largest summed time; achieved = its
+    algorithmic FLOPs (2*MAC per launch) / its summed launch durations (= FLOPs per
+    launch / average launch duration)."""
+    bs = pipe.eng.slices(pipe.B)[0]
+    fr = frames[:bs].contiguous()
+    out = pipe.eng.alloc_out(bs)
     best = None
     for _ in range(reps):
-        ops = pipe.eng.profile(frames, pipe.out)
+        ops = pipe.eng.profile(fr, out)
         if best is None:
             best = [list(o) for o in ops]
         else:
@@ -118,7 +123,8 @@ def conv_roofline(pipe, frames, precision, reps=3):
     top = sorted(best, key=lambda o: -o[1])[:6]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
-            "traffic": load_traffic(name, pipe.B, precision),
+            "traffic": load_traffic(name, bs, precision),
+            "launch_batch": bs,
             "kernel": f"{name}: {n} launches/forward, avg {ms / n:.4f} ms, avg {flops / n / 1e9:.2f} GFLOP/launch",
             "all_conv": {"launches": len(conv), "ms": round(all_ms, 3), "tflops": round(all_fl / all_ms / 1e9, 1)},
             "per_kernel": {k: {"launches": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / v[1] / 1e9, 1)}

@@ -146,6 +146,22 @@ const char* tv_engine_op_label(tv_engine* e, int32_t i) {
   return e->e.plan.ops[i].label.c_str();
 }
 
+int tv_engine_slices(tv_engine* e, int32_t B, int32_t* n, int32_t sb[2]) {
+  TV_GUARD({
+    if (!e || !n || !sb || B < 1) { set_error("bad argument"); return TV_EINVAL; }
+    if (e->e.slices > 1 && B >= 2 * e->e.slice_min) {
+      *n = 2;
+      sb[0] = B / 2;
+      sb[1] = B - B / 2;
+    } else {
+      *n = 1;
+      sb[0] = B;
+      sb[1] = 0;
+    }
+    return TV_OK;
+  })
+}
+
 const char* tv_engine_op_kernel(tv_engine* e, int32_t B, int32_t i) {
   if (!e || i < 0 || i >= (int)e->e.plan.ops.size()) return "";
   return e->e.op_kernel(B, i);

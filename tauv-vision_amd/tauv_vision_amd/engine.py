@@ -42,6 +42,13 @@ class NativeEngine:
         g = self.geom
         return g["out_h"], g["out_w"], g["out_cpad"]
 
+    def slices(self, batch):
+        """Frame counts of the concurrent slices a forward of `batch` frames launches."""
+        n = ctypes.c_int32()
+        sb = (ctypes.c_int32 * 2)()
+        _lib.check(_lib.lib().tv_engine_slices(self._h, batch, ctypes.byref(n), sb), "slices")
+        return [sb[i] for i in range(n.value)]
+
     def alloc_out(self, batch):
         oh, ow, oc = self.out_shape_per_frame
         return torch.empty((batch, oh, ow, oc), dtype=torch.float32, device=self.device)

@@ -11,6 +11,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 TV_PROFILE_OUT=$O/ops.json timeout -k 10 400 python bench.py > $O/bench.log 2>&1
 tail -1 $O/bench.log | cut -c1-600
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o rprof --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-b1 > $O/prof.log 2>&1
+# PMC passes: one forward of the bench workload (B=64 u8 frames = two concurrent 32-frame slices)
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c -d $O/pmc -o $c --output-format csv -- python tools/prof_forward.py --iters 1 > $O/pmc/$c.log 2>&1
 done

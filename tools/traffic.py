@@ -40,7 +40,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch")
     ap.add_argument("write")
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=32, help="frames per launch (a B=64 forward = two 32-frame slices)")
     ap.add_argument("--precision", default="fp16")
     ap.add_argument("-o", "--out", default="profiles/hbm_traffic.json")
     a = ap.parse_args()

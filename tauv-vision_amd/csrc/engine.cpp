@@ -242,20 +242,14 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
       cu_count = ncu;
   }
   if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_CUS")) cu_count = std::max(8, std::min(cu_count, std::atoi(env)));
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_SLICES")) slices = std::atoi(env);
-  // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
-  if (stem_mode && dtype != F32)
-    for (size_t i = 0; i + 1 < plan.ops.size(); ++i)
-      if (plan.ops[i].kind == OP_PREP && plan.ops[i + 1].kind == OP_CONV && plan.ops[i + 1].segs.size() == 1 &&
-          plan.ops[i + 1].segs[0].row_expand == 7 && plan.ops[i + 1].N <= 128 && plan.ops[i + 1].N % 8 == 0 &&
-          plan.ops[i + 1].act == 1) {
-        stem_op = (int)i + 1;
-        break;
-      }
+  if (const char* env = std::getenv("TV_STAGGER")) stagger = std::atoi(env);
   packed.resize(plan.ops.size());
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     rc = pack_op(i);
@@ -467,7 +461,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const size_t src_bytes = (size_t)B * cs.H * cs.W * cs.ldc * esz;
       if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand && cs.C == 128 &&
           cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && src_bytes < (1ull << 31) &&
-          p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2) {
+          p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix) {
         const int res = res2 ? 1 : 0;
         const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16), t32 = conv3x3_tiles(B, cs.H, cs.W, 32);
         const int tw = t32 <= t16 ? 32 : 16;
@@ -689,11 +683,11 @@ int Engine::get_side(hipStream_t s, SideStream** out) {
   return TV_OK;
 }
 
-int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStream_t s) {
+int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStream_t s, size_t op0, size_t op1) {
   Workspace* ws = nullptr;
   int rc = get_workspace(B, s, &ws);
   if (rc) return rc;
-  for (size_t i = 0; i < plan.ops.size(); ++i) {
+  for (size_t i = op0; i < plan.ops.size() && i < op1; ++i) {
     rc = run_op(i, ws, input, input_u8, out, s);
     if (rc) return rc;
   }
@@ -734,11 +728,17 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
     const int B1 = B / 2;
     const size_t in_frame = input_u8 ? (size_t)desc.in_h * desc.in_w * 3 : (size_t)3 * desc.in_h * desc.in_w * 4;
     const size_t out_frame = (size_t)plan.out_h * plan.out_w * plan.out_cpad;
+    // optional staggered start (env TV_STAGGER = k): the side slice begins once the first has
+    // run its first k ops; measured no better than k = 0 (the persistent large-layer kernels
+    // occupy every CU, so the other slice's small launches cannot slip in beside them)
+    const size_t k = (size_t)stagger;
+    rc = run_all(input, input_u8, B1, out, s, 0, k);
+    if (rc) return rc;
     TV_HIP(hipEventRecord(ss->fork, s));
     TV_HIP(hipStreamWaitEvent(ss->s, ss->fork, 0));
-    rc = run_all(input, input_u8, B1, out, s);
-    if (rc) return rc;
     rc = run_all((const char*)input + B1 * in_frame, input_u8, B - B1, out + B1 * out_frame, ss->s);
+    if (rc) return rc;
+    rc = run_all(input, input_u8, B1, out, s, k);
     if (rc) return rc;
     TV_HIP(hipEventRecord(ss->join, ss->s));
     TV_HIP(hipStreamWaitEvent(s, ss->join, 0));

@@ -55,6 +55,7 @@ struct Engine {
   size_t weight_bytes = 0;
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
   int pipe_mode = 1;           // -1 auto (>= 256 tiles), 0 never, 1 whenever representable (env TV_CONV_PIPE)
+  int conv3_min_pix = 100;     // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)
   int s2_mode = 1;             // stride-2 halo kernel for eligible fp16/bf16 layers (env TV_CONV3S2=0 off)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
   int cu_count = 256;          // compute units (persistent grids)
@@ -69,6 +70,7 @@ struct Engine {
   // overlap the other half's large ones (env TV_SLICES=1 off)
   int slices = 2;
   int slice_min = 8;
+  int stagger = 0;   // the side slice starts after this many ops of the first (env TV_STAGGER)
   struct SideStream {
     hipStream_t s = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
@@ -93,7 +95,8 @@ struct Engine {
   int pack_op(size_t i);
   int make_workspace(int B, Workspace* ws);
   int run_op(size_t i, Workspace* ws, const void* input, int input_u8, float* out, hipStream_t s);
-  int run_all(const void* input, int input_u8, int B, float* out, hipStream_t s);
+  int run_all(const void* input, int input_u8, int B, float* out, hipStream_t s, size_t op0 = 0,
+              size_t op1 = (size_t)-1);
   int get_side(hipStream_t s, SideStream** out);
 };
 

@@ -1,0 +1,279 @@
+// ConvTranspose2d(k = s, stride = s) + pad_to_match + skip add (gfx950, fp16 / bf16) — the
+// IDAUp / IDAUpReverse up-path of the reference: `f_i + pad_to_match(up(project(x)), f_i)`
+// (dla.py:265-284, 340-357, pad_to_match :195-209, including its H/W-swapped F.pad quirk,
+// folded into the target shift (sy, sx) by the planner).
+//
+// A k = s transposed conv is a per-pixel linear map: input pixel (iy, ix) produces the s x s
+// block of target pixels (iy*s + py + sy, ix*s + px + sx), one 128-channel GEMM row per phase
+// (py, px). Per phase it is a GEMM [input pixels] x [128 x 128], K = 128, and the pass is bound
+// by HBM: per input pixel and phase it reads 256 B of skip tensor and writes 256 B (the 256 B of
+// input pixel come from L2 after the first phase). The generic implicit GEMM staged that
+// through a 3-slot LDS ring and an fp32 LDS epilogue per 256-pixel tile (2.7 TB/s). Here:
+//  * a 256-thread workgroup owns one phase and a run of 32-pixel tiles; the phase's weights
+//    (128 x 128, 34 KiB with a conflict-free 272 B row pitch) move to LDS once;
+//  * each wave streams its own tiles with no barrier: the MFMA B operand (8 x 16 B of the
+//    pixel's channels per lane) and the skip chunks the epilogue adds are loaded straight
+//    into registers one tile ahead — issued before the previous tile's stores, so waiting for
+//    them never waits for those stores (vector memory completes in issue order);
+//  * the epilogue works on the accumulators in place (bias, + skip in fp32, one rounding,
+//    v_permlane32_swap into 16-byte stores), in the same arithmetic order as conv_pipe's
+//    mode-1 epilogue: (acc + bias) + skip.
+#include "conv_common.h"
+
+namespace tv {
+namespace convt {
+
+constexpr int NT = 768;        // 12 waves = 6 pixel streams x 2 output-channel halves
+constexpr int NW = NT / 64;
+constexpr int NS = NW / 2;     // pixel streams per workgroup
+constexpr int C = 128;         // output channels per phase (4 MFMA row tiles)
+constexpr int KJ = 8;          // K = 128 input channels = 8 MFMA k-steps of 16
+constexpr int WPITCH = 272;    // LDS weight row pitch (bytes): odd multiple of 16 -> no bank conflicts
+constexpr int PW = C * WPITCH; // one phase's weights
+constexpr int NPG = 4;         // phases per workgroup on large inputs: the input tile is loaded once for all
+template <int NP>
+constexpr int lds_bytes() { return NP * (PW + C * 4); }
+
+template <typename T>
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, t2{(T)a, (T)b});
+}
+template <typename T>
+__device__ __forceinline__ float lo_f(unsigned u) {
+  return (float)__builtin_bit_cast(T, (uint16_t)(u & 0xffffu));
+}
+template <typename T>
+__device__ __forceinline__ float hi_f(unsigned u) {
+  return (float)__builtin_bit_cast(T, (uint16_t)(u >> 16));
+}
+
+struct XSet {
+  uint4 x[KJ];   // B operand: input pixel channels 16j + 8*lh .. +8
+};
+struct ASet {
+  uint4 a[4];    // skip chunks j: channels 64*half + 16j + 8*lh .. +8 at the target pixel
+};
+
+// A workgroup owns NP consecutive phases of the s*s and a run of 32-pixel input tiles; per tile
+// a wave loads the input operand once and runs the NP phases, the skip chunks of the next phase
+// step in flight under the current one (NP = 4 on large inputs; NP = 1 spreads small inputs over
+// s*s times more workgroups).
+template <typename T, int NP>
+__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(3, 3))) void convt_add(ConvTParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(NP == 1 || NP % 2 == 0, "phase group");
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int half = wave & 1, stream = wave >> 1;  // output channels [64 half, +64), pixel stream
+  const int group = blockIdx.x / p.nchunks;
+  const int chunk = blockIdx.x - group * p.nchunks;
+  const int phase0 = group * NP;
+
+  // ---- the group's weights and bias into LDS (rows n = phase*C + co of the packed [N][Kpad])
+  {
+    const char* wsrc = reinterpret_cast<const char*>(p.weight) + (size_t)phase0 * C * p.Kpad * sizeof(T);
+    for (int i = tid; i < NP * C * 16; i += NT) {
+      const int r = i >> 4, c = i & 15;  // r = phase-in-group * C + co
+      *reinterpret_cast<uint4*>(smem + r * WPITCH + c * 16) =
+          *reinterpret_cast<const uint4*>(wsrc + (size_t)r * p.Kpad * sizeof(T) + c * 16);
+    }
+    float* lb = reinterpret_cast<float*>(smem + NP * PW);
+    for (int i = tid; i < NP * C; i += NT) lb[i] = p.bias[phase0 * C + i];
+  }
+  __syncthreads();
+
+  // GEMM rows are input pixels (b, iy, ix)
+  const int hw = p.h * p.w;
+  const int M = p.B * hw;
+  const int mt = (M + 31) / 32;
+  const int t_begin = (chunk * NS + stream) * p.tpw;
+  const int t_end = min(t_begin + p.tpw, mt);
+  if (t_begin >= t_end) return;
+
+  // target element offset (channel 0) of this lane's pixel in tile t for phase ph, or -1
+  auto target = [&](int t, int ph) __attribute__((always_inline)) -> long long {
+    const int m = t * 32 + l32;
+    if (m >= M) return -1;
+    const int phase = phase0 + ph;
+    const int py = phase / p.s, px = phase - py * p.s;
+    const int b = m / hw;
+    const int rem = m - b * hw;
+    const int iy = rem / p.w, ix = rem - iy * p.w;
+    const int Y = iy * p.s + py + p.sy, X = ix * p.s + px + p.sx;
+    if (Y >= p.tH || X >= p.tW) return -1;
+    return ((long long)(b * p.tH + Y) * p.tW + X);
+  };
+  auto load_x = [&](int t, XSet& S) __attribute__((always_inline)) {
+    const int m = t * 32 + l32;
+    const size_t sp = (size_t)(m < M ? m : 0);
+    const T* src = reinterpret_cast<const T*>(p.src) + sp * p.src_ldc + 8 * lh;
+#pragma unroll
+    for (int j = 0; j < KJ; ++j) S.x[j] = gload16(src + 16 * j);
+  };
+  auto load_a = [&](int t, int ph, ASet& S) __attribute__((always_inline)) {
+    if (p.ablate & 4) return;
+    const long long tg = target(t, ph);
+    const T* add = reinterpret_cast<const T*>(p.add) + (tg < 0 ? 0 : tg) * p.add_ldc + 64 * half + 8 * lh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S.a[q] = gload16(add + 16 * q);  // q = 2ii + m -> channel 64 half + 16q + 8lh
+  };
+
+  auto compute_store = [&](int t, int ph, const XSet& X, const ASet& A) __attribute__((always_inline)) {
+    const char* wl = smem + ph * PW + (64 * half + l32) * WPITCH + lh * 16;
+    const float* lb = reinterpret_cast<const float*>(smem + NP * PW) + ph * C + 64 * half;
+    f32x16 acc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) acc[i] = f32x16{};
+    // weight fragments one k-step at a time (bounded live set)
+#pragma unroll
+    for (int j = 0; j < KJ; ++j) {
+      uint4 wv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) wv[i] = *reinterpret_cast<const uint4*>(wl + i * 32 * WPITCH + j * 32);
+      if (!(p.ablate & 2)) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) Mfma<T>::run(wv[i], X.x[j], acc[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const long long tg = target(t, ph);
+    T* out = reinterpret_cast<T*>(p.out) + (tg < 0 ? 0 : tg) * p.out_ldc + 64 * half;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        float v[2][4];
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int G2 = 2 * m + gg;
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(lb + 32 * i + 8 * G2 + 4 * lh);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[gg][e] = acc[i][4 * G2 + e] + bb[e];
+        }
+        // registers -> 16-byte chunk: lanes 0-31 channels 32i+16m+0..7, lanes 32-63 +8..15
+        float f[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][e]), __float_as_uint(v[1][e]), false,
+                                                          false);
+          f[e] = __uint_as_float(r[0]);
+          f[4 + e] = __uint_as_float(r[1]);
+        }
+        unsigned o[4];
+        const uint4 sk = A.a[2 * i + m];
+        const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pack2<T>(lo_f<T>(sw[e]) + f[2 * e], hi_f<T>(sw[e]) + f[2 * e + 1]);
+        if (tg >= 0 && !(p.ablate & 1)) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
+      }
+  };
+
+  // Steps (tile, phase) in order; the operands of the next step are loaded before the current
+  // step's stores are issued (vector memory completes in issue order). Register sets
+  // alternate: x by tile parity, skip by step parity (NP is 1 or even) -> unrolled by 2 tiles.
+  XSet x0, x1;
+  ASet a0, a1;
+  load_x(t_begin, x0);
+  load_a(t_begin, 0, a0);
+  if constexpr (NP == 1) {
+    // single phase: both sets alternate per tile
+    for (int t = t_begin; t < t_end; t += 2) {
+      if (t + 1 < t_end) {
+        load_x(t + 1, x1);
+        load_a(t + 1, 0, a1);
+      }
+      compute_store(t, 0, x0, a0);
+      if (t + 1 >= t_end) break;
+      if (t + 2 < t_end) {
+        load_x(t + 2, x0);
+        load_a(t + 2, 0, a0);
+      }
+      compute_store(t + 1, 0, x1, a1);
+    }
+  } else {
+    // NP (even) phases per tile: skip sets alternate per phase (even phases a0), x per tile
+    auto tile = [&](int t, XSet& xc, XSet& xn) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ph = 0; ph < NP; ph += 2) {
+        load_a(t, ph + 1, a1);
+        compute_store(t, ph, xc, a0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ph + 2 < NP) {
+          load_a(t, ph + 2, a0);
+        } else if (t + 1 < t_end) {
+          load_x(t + 1, xn);
+          load_a(t + 1, 0, a0);
+        }
+        compute_store(t, ph + 1, xc, a1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    for (int t = t_begin; t < t_end; t += 2) {
+      tile(t, x0, x1);
+      if (t + 1 >= t_end) break;
+      tile(t + 1, x1, x0);
+    }
+  }
+}
+
+template <typename T, int NP>
+static int launch_t(const ConvTParams& p, hipStream_t s) {
+  auto k = convt_add<T, NP>;
+  constexpr int lds = lds_bytes<NP>();
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) {
+      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+      return 3;
+    }
+    attr = true;
+  }
+  const int groups = p.s * p.s / NP;
+  hipLaunchKernelGGL(k, dim3(groups * p.nchunks), dim3(NT), lds, s, p);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace convt
+
+bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc) {
+  return cin == convt::KJ * 16 && cout == convt::C && src_ldc % 8 == 0 && add_ldc % 8 == 0 && out_ldc % 8 == 0;
+}
+
+// tiles per wave: about one resident 8-wave workgroup per CU over the whole launch, >= 2 tiles per wave
+void convt_schedule(ConvTParams& p, int cu_count) {
+  const long M = (long)p.B * p.h * p.w;
+  const long mt = (M + 31) / 32;
+  const long waves_target = (long)convt::NS * cu_count;  // pixel streams
+  // phase groups of 4 once every wave of the launch gets >= 2 tiles that way
+  p.np = (p.s * p.s % convt::NPG == 0 &&
+          mt * (p.s * p.s / convt::NPG) >= 2 * waves_target) ? convt::NPG : 1;
+  const long groups = (long)p.s * p.s / p.np;
+  long per_group = (waves_target + groups - 1) / groups;
+  long tpw = (mt + per_group - 1) / per_group;
+  if (tpw < 1) tpw = 1;
+  p.tpw = (int)tpw;
+  p.nchunks = (int)((mt + convt::NS * tpw - 1) / (convt::NS * tpw));
+}
+
+int launch_convt(const ConvTParams& p, int dtype, hipStream_t s) {
+  if (p.tpw < 1 || p.nchunks < 1 || p.s < 1) {
+    set_error("convt: not scheduled");
+    return 1;
+  }
+  using namespace convt;
+  if (p.np != 1 && p.np != NPG) {
+    set_error("convt: bad phase group");
+    return 1;
+  }
+  if (dtype == F16) return p.np == NPG ? launch_t<_Float16, NPG>(p, s) : launch_t<_Float16, 1>(p, s);
+  if (dtype == BF16) return p.np == NPG ? launch_t<__bf16, NPG>(p, s) : launch_t<__bf16, 1>(p, s);
+  set_error("convt: fp16/bf16 only");
+  return 1;
+}
+
+}  // namespace tv

@@ -242,6 +242,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
       cu_count = ncu;
   }
   if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_C3_TW")) c3_tw_force = std::atoi(env) == 16 ? 16 : std::atoi(env) == 32 ? 32 : 0;
   if (const char* env = std::getenv("TV_CUS")) cu_count = std::max(8, std::min(cu_count, std::atoi(env)));
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
@@ -250,6 +251,15 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_SLICES")) slices = std::atoi(env);
   if (const char* env = std::getenv("TV_STAGGER")) stagger = std::atoi(env);
+  // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
+  if (stem_mode && dtype != F32)
+    for (size_t i = 0; i + 1 < plan.ops.size(); ++i)
+      if (plan.ops[i].kind == OP_PREP && plan.ops[i + 1].kind == OP_CONV && plan.ops[i + 1].segs.size() == 1 &&
+          plan.ops[i + 1].segs[0].row_expand == 7 && plan.ops[i + 1].N <= 128 && plan.ops[i + 1].N % 8 == 0 &&
+          plan.ops[i + 1].act == 1) {
+        stem_op = (int)i + 1;
+        break;
+      }
   packed.resize(plan.ops.size());
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     rc = pack_op(i);
@@ -464,7 +474,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
           p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix) {
         const int res = res2 ? 1 : 0;
         const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16), t32 = conv3x3_tiles(B, cs.H, cs.W, 32);
-        const int tw = t32 <= t16 ? 32 : 16;
+        const int tw = c3_tw_force ? c3_tw_force : t32 <= t16 ? 32 : 16;
         const int mt = tw == 32 ? t32 : t16;
         long total = (long)mt * p.ntiles;
         int grid = (int)std::min<long>(total, cu_count);

@@ -55,6 +55,7 @@ struct Engine {
   size_t weight_bytes = 0;
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
   int pipe_mode = 1;           // -1 auto (>= 256 tiles), 0 never, 1 whenever representable (env TV_CONV_PIPE)
+  int c3_tw_force = 0;         // conv3x3 tile width override (env TV_C3_TW = 16 / 32)
   int conv3_min_pix = 100;     // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)
   int s2_mode = 1;             // stride-2 halo kernel for eligible fp16/bf16 layers (env TV_CONV3S2=0 off)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)

@@ -205,3 +205,28 @@ def test_large_batch_property_fp16():
     assert torch.equal(many, many[:1].expand(64, -1, -1, -1))
     scale = max(1.0, float(one.abs().max()))
     assert float((many[:1] - one).abs().max()) <= TOL["fp16"] * scale
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_kernel_selection_full_size(precision):
+    """The throughput path runs on the hand-written gfx950 kernels it was designed around (a
+    silent fall-back to the generic implicit GEMM would still pass every parity test): at
+    B = 64 (two 32-frame slices) the stem, the stride-2 and stride-1 halo kernels, the residual
+    k-step variant, the fused heads and the ConvTranspose kernel must all be selected."""
+    import tauv_vision_amd as tv
+    name = "r18_c128_b1_480x640"
+    model, oc, mc, case = build(name, precision)
+    eng = model.engine(torch.device("cuda", 0), 480, 640)
+    bs = eng.slices(64)
+    assert bs == [32, 32]
+    frames = torch.zeros((bs[0], 480, 640, 3), dtype=torch.uint8, device="cuda")
+    ops = eng.profile(frames, eng.alloc_out(bs[0]))
+    kern = {label: k for label, _, _, k in ops}
+    assert kern["backbone.dla_down.projection_layer.0"].startswith("tv::stem::stem_conv<"), kern
+    assert kern["backbone.dla_down.block_layers.0.conv1"].startswith("tv::c3s2::conv3x3s2<")
+    assert kern["backbone.dla_down.block_layers.0.conv2+conv_residual"].startswith("tv::c3::conv3x3<")
+    assert kern["backbone.dla_down.block_layers.0.conv2+conv_residual"].endswith(", 1>")  # RES k-steps
+    assert kern["heads.*.0 (stacked) + LeakyReLU"].startswith("tv::c3::conv3x3<")
+    assert kern["heads.*.2 (block-diagonal) -> fp32 NHWC"] == "(fused into the 3x3 heads)"
+    assert kern["backbone.ida_up_reverse.upsample_layers.0+pad_to_match+add"].startswith("tv::convt::convt_add<")
+    assert kern["backbone.multi_ida_up.ida_up_layers.0.output_layers.0.0"].startswith("tv::c3::conv3x3<")

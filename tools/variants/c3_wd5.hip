@@ -23,8 +23,7 @@
 //  * two halo buffers (the next channel block — or the next tile's first — streams in during
 //    taps 0..5 of the current one), a 3-slot weight ring (8 KiB per k-step from a k-step-major,
 //    pre-swizzled copy of the weights: each wave's 1 KiB piece is contiguous; loaded into
-//    registers five k-steps ahead (4 register sets) and written with ds_write_b128 two steps
-//    before use — deep enough for the few-tile layers that stream weights from HBM), one raw
+//    registers three k-steps ahead and written with ds_write_b128 one step later), one raw
 //    s_barrier per k-step with an exact counted vmcnt;
 //  * fragment reads run one 16-deep sub-step ahead of the MFMAs (6 ds_read_b128 per half
 //    k-step, two register sets) and the k-step's LDS-DMA pieces are issued between MFMA pairs;

@@ -408,16 +408,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   halo_piece(IC<3>{}, 0, 0);
   halo_piece(IC<4>{}, 0, 0);
   halo_piece(IC<5>{}, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);  // the counted wait below needs the halo issued first
   // weights: k-steps 0, 1 into ring slots 0, 1; k-steps 2, 3, 4 in flight in sets 2, 3, 0
+  // (S_tot >= SPTK > 5). Every VMEM operation of the main loop is issued unconditionally —
+  // past the end of the list the weight loads re-read the last tile's k-steps and the halo
+  // pieces reload the current tile into the idle buffer — so that the compiler's own vmcnt
+  // for each weight ds_write is exact: a conditional load makes it fall back to vmcnt(0),
+  // which drains the halo pieces and weight loads issued since (measured: ~20% of the layer).
   w_load(wreg[0]);
-  if (S_tot > 1) w_load(wreg[1]);
+  w_load(wreg[1]);
   *reinterpret_cast<u32x4*>(smem + OFF_W + wave * 1024 + lane * 16) = wreg[0];
-  if (S_tot > 1) *reinterpret_cast<u32x4*>(smem + OFF_W + WSLOT + wave * 1024 + lane * 16) = wreg[1];
-  if (S_tot > 2) w_load(wreg[2]);
-  if (S_tot > 3) w_load(wreg[3]);
-  if (S_tot > 4) w_load(wreg[0]);
+  *reinterpret_cast<u32x4*>(smem + OFF_W + WSLOT + wave * 1024 + lane * 16) = wreg[1];
+  w_load(wreg[2]);
+  w_load(wreg[3]);
+  w_load(wreg[0]);
   // the halo (issued first) landed; the weights of k-steps 2..4 may stay in flight
-  wait_vm_n((S_tot > 2) + (S_tot > 3) + (S_tot > 4));
+  wait_vm<3>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -447,18 +453,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // Weights of k-step s+1 were written to LDS at step s-1 (lgkmcnt + barrier below); halo and
     // residual data arrive by LDS-DMA and are waited for with an exact vmcnt: the count of
     // vector-memory operations issued after the last piece the next k-step reads. A weight load
-    // was issued at step q iff q + 3 < S_tot; within a step the order is weight load, halo piece
+    // is issued at every step q >= 0; within a step the order is weight load, halo piece
     // (taps 0..5, next channel block), residual piece (RES, taps 1..4, this channel block).
     //  * tap 8 without RES / residual step (tap 9): the next k-step reads the NEXT channel
     //    block's halo (last piece at tap 5): younger = the weight loads of taps 6, 7 (and 8);
     //  * tap 8 with RES: the residual step reads this block's residual input (last piece at
     //    tap 4): younger = weight loads of taps 5, 6, 7 + the tap-5 halo piece.
     static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
-    auto wl = [&](int q) { return q >= 0 && q + 5 < S_tot ? 1 : 0; };
+    auto wl = [&](int q) { return q >= 0 ? 1 : 0; };
     unsigned long long tw0 = 0;
     if (p.stamps) tw0 = __builtin_amdgcn_s_memtime();
     if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 2) + wl(s - 1) : 0);
-    if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) + (nxt_exists ? 1 : 0) : 0);
+    if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
     if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -475,7 +481,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
     constexpr int PAR = decltype(par)::value;  // s % 4 (36 or 40 k-steps per tile: static)
-    if (s + 5 < S_tot) w_load(wreg[(PAR + 1) & 3]);   // k-step s+5 (that set's k-step s+1 is in LDS)
+    w_load(wreg[(PAR + 1) & 3]);   // k-step s+5 (that set's k-step s+1 is in LDS)
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
@@ -483,10 +489,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
     read_one(IC<2>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<3>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    // k-step s+2 (loaded at step s-1) into its ring slot: it last held k-step s-1, read
-    // completely before this step's barrier
-    if (s + 2 < S_tot)
-      *reinterpret_cast<u32x4*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = wreg[(PAR + 2) & 3];
+    // k-step s+2 (loaded at step s-3) into its ring slot: it last held k-step s-1, read
+    // completely before this step's barrier (past the end: an unread slot)
+    *reinterpret_cast<u32x4*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = wreg[(PAR + 2) & 3];
     if constexpr (TAP == 0) {
       if (nxt_exists && nxt_newtile) {
         int fr, y0, x0, nt;
@@ -499,7 +504,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     if constexpr (TAP < HTAPS)
-      if (nxt_exists) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);
+      halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);  // (no next block: the idle buffer)
     if constexpr (RES && TAP >= 1 && TAP <= RPW) res_piece(TAP - 1, cur_fr, cur_y0, cur_x0, cb);
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<3>{}, IC<FIRST>{}, H0);

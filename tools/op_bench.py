@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--precision", default="fp16")
     ap.add_argument("--match", default="")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--dump", default="", help="write the op labels as JSON (tools/stamps.py)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     model, oc, sd = build_model(a.precision, dev)
@@ -32,6 +33,10 @@ def main():
         ops = eng.profile(frames, out)
         best = [list(o) for o in ops] if best is None else [[b[0], min(b[1], o[1]), b[2], b[3]] for b, o in zip(best, ops)]
     tot = sum(o[1] for o in best)
+    if a.dump:
+        import json
+        with open(a.dump, "w") as f:
+            json.dump([{"op": o[0]} for o in best], f)
     sel = [o for o in best if a.match in o[0]]
     for o in sel:
         print(f"{a.tag} {o[1]:8.4f} ms {o[2] / max(o[1], 1e-9) / 1e9:8.1f} TF  {o[3][:40]:40s} {o[0][:60]}")

@@ -453,19 +453,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // Weights of k-step s+1 were written to LDS at step s-1 (lgkmcnt + barrier below); halo and
     // residual data arrive by LDS-DMA and are waited for with an exact vmcnt: the count of
     // vector-memory operations issued after the last piece the next k-step reads. A weight load
-    // is issued at every step q >= 0; within a step the order is weight load, halo piece
-    // (taps 0..5, next channel block), residual piece (RES, taps 1..4, this channel block).
+    // is issued at every step q >= 0; within a step the order is halo piece (taps 0..5, next
+    // channel block), residual piece (RES, taps 1..4, this channel block), weight load.
     //  * tap 8 without RES / residual step (tap 9): the next k-step reads the NEXT channel
-    //    block's halo (last piece at tap 5): younger = the weight loads of taps 6, 7 (and 8);
+    //    block's halo (last piece at tap 5): younger = the weight loads of taps 5, 6, 7 (and 8);
     //  * tap 8 with RES: the residual step reads this block's residual input (last piece at
-    //    tap 4): younger = weight loads of taps 5, 6, 7 + the tap-5 halo piece.
+    //    tap 4): younger = weight loads of taps 4, 5, 6, 7 + the tap-5 halo piece.
     static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
     auto wl = [&](int q) { return q >= 0 ? 1 : 0; };
     unsigned long long tw0 = 0;
     if (p.stamps) tw0 = __builtin_amdgcn_s_memtime();
-    if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 2) + wl(s - 1) : 0);
-    if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
-    if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
+    if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
+    if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
+    if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -481,7 +481,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
     constexpr int PAR = decltype(par)::value;  // s % 4 (36 or 40 k-steps per tile: static)
-    w_load(wreg[(PAR + 1) & 3]);   // k-step s+5 (that set's k-step s+1 is in LDS)
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
@@ -512,6 +511,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<0>{}, IC<false>{}, H1);
+    // k-step s+5 into the set whose k-step s+1 went to LDS at step s-1. Issued here, after the
+    // halo/residual pieces and away from the barrier where all 8 waves issue at once (-4%)
+    w_load(wreg[(PAR + 1) & 3]);
     if (do_r) {
       read_one(IC<0>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<1>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);

@@ -42,7 +42,8 @@ constexpr int WSLOT = BN * 64;    // weights of one k-step: 128 rows x 64 B
 constexpr int RING = 3;
 constexpr int OFF_W = NBUF * HBUF;
 constexpr int OFF_B = OFF_W + RING * WSLOT;
-constexpr int LDS = OFF_B + BN * 4;
+constexpr int OFF_D = OFF_B + BN * 4;  // 1 KiB sink of the 6th halo piece of waves 4-7 (OOB: zeros)
+constexpr int LDS = OFF_D + 1024;
 static_assert(LDS <= 160 * 1024, "LDS budget");
 static_assert(HPIECES * 64 >= HPIX * 5, "halo pieces");
 constexpr int HPW = 6;            // halo pieces per wave: waves 0-3 issue 6, waves 4-7 issue 5 (44)
@@ -57,6 +58,7 @@ constexpr int J_TAP[9] = {0, 2, 6, 8, 1, 7, 3, 5, 4};
 typedef __attribute__((address_space(3))) char lds_char;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+__device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
 __device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
                                     int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
 
@@ -85,7 +87,8 @@ __device__ __forceinline__ void wait_vm_n(int n) {
     case 7: wait_vm<7>(); break;
     case 8: wait_vm<8>(); break;
     case 9: wait_vm<9>(); break;
-    default: wait_vm<10>(); break;
+    case 10: wait_vm<10>(); break;
+    default: wait_vm<11>(); break;
   }
 }
 
@@ -155,7 +158,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     r.w = 0x00020000;
     return r;
   };
-  const char* wts = reinterpret_cast<const char*>(p.weight) + wave * 1024 + lane * 16;
 
   auto tile_of = [&](int idx, int& fr, int& y0, int& x0) __attribute__((always_inline)) {
     const int t = first + idx * stride;
@@ -180,26 +182,37 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const int pr = pb < 2 ? 1 : 0, pc = (pb & 1) == 0 ? 1 : 0;  // PB_P, PB_Q
     const i32x4 rs = rsrc_of(fr);
     lds_char* base = lds + buf * HBUF + pbase * 1024;
+    // every wave issues HPW pieces: unconditional VMEM keeps the compiler's vmcnt for the weight
+    // ds_write exact (a conditional load makes it vmcnt(0)); waves 4-7 send their 6th, all-OOB
+    // piece to the LDS sink
 #pragma unroll
     for (int i = 0; i < HPW; ++i) {
-      if (i < npw) {
-        const unsigned gq = hgeo[i];
-        const int hy = (int)(gq >> 16), hx = (int)((gq >> 8) & 0xff);
-        const int y = 2 * y0 - pr + 2 * hy, x = 2 * x0 - pc + 2 * hx;
-        const bool ok = gq != ~0u && hy < TH + pr && hx < TW + pc && (unsigned)y < (unsigned)H &&
-                        (unsigned)x < (unsigned)W;
-        const unsigned off = ok ? ((unsigned)y * (unsigned)W + (unsigned)x) * pix_bytes + (gq & 0xff) * 16u : 0x80000000u;
-        raw_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(base + i * 1024), 16, (int)off,
-                            cb * CBK * (int)sizeof(T), 0, 0);
-      }
+      const unsigned gq = hgeo[i];
+      const int hy = (int)(gq >> 16), hx = (int)((gq >> 8) & 0xff);
+      const int y = 2 * y0 - pr + 2 * hy, x = 2 * x0 - pc + 2 * hx;
+      const bool ok = gq != ~0u && hy < TH + pr && hx < TW + pc && (unsigned)y < (unsigned)H &&
+                      (unsigned)x < (unsigned)W;
+      const unsigned off = ok ? ((unsigned)y * (unsigned)W + (unsigned)x) * pix_bytes + (gq & 0xff) * 16u : 0x80000000u;
+      lds_char* dst = i < npw ? base + i * 1024 : lds + OFF_D;
+      raw_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, (int)off, cb * CBK * (int)sizeof(T), 0, 0);
     }
   };
 
   // ---- register-staged weights (as conv3x3.hip): k-step q loaded at step q-3, written at q-2
+  // through a buffer resource: one lane-offset VGPR, the k-step offset in an SGPR
   int wc_in = 0;
-  u32x4 wreg[2];
+  u32x4 wreg[4];  // k-step q is loaded at step q-5 into set q % 4, written to LDS at step q-2
+  i32x4 wrsrc;
+  {
+    const unsigned long long a = (unsigned long long)p.weight;
+    wrsrc.x = (int)(unsigned)a;
+    wrsrc.y = (int)(unsigned)(a >> 32);
+    wrsrc.z = SPT * WSLOT;
+    wrsrc.w = 0x00020000;
+  }
+  const int wvoff = wave * 1024 + lane * 16;
   auto w_load = [&](u32x4& dst) __attribute__((always_inline)) {
-    dst = *(g_cu32x4*)(wts + (size_t)wc_in * WSLOT);
+    dst = raw_buffer_load_v4(wrsrc, wvoff, wc_in * WSLOT, 0);
     if (++wc_in == SPT) wc_in = 0;
   };
 
@@ -272,12 +285,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   tile_of(0, cur_fr, cur_y0, cur_x0);
   issue_block(cur_fr, cur_y0, cur_x0, 0, 0, 0);
   issue_block(cur_fr, cur_y0, cur_x0, 0, 1, 1);
+  __builtin_amdgcn_sched_barrier(0);  // the counted wait below needs the halos issued first
   w_load(wreg[0]);
   w_load(wreg[1]);
   *reinterpret_cast<u32x4*>(smem + OFF_W + wave * 1024 + lane * 16) = wreg[0];
   *reinterpret_cast<u32x4*>(smem + OFF_W + WSLOT + wave * 1024 + lane * 16) = wreg[1];
+  w_load(wreg[2]);
+  w_load(wreg[3]);
   w_load(wreg[0]);
-  wait_vm<1>();  // both halos landed (issued before the weights); k-step 2's weights may stay in flight
+  wait_vm<3>();  // both halos landed (issued before the weights); k-steps 2..4 may stay in flight
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -301,13 +317,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     constexpr int CB = decltype(cbc)::value, J = decltype(jc)::value;
     constexpr bool BOUNDARY = J == 3 || J == 5 || J == 7 || J == 8;  // the next k-step starts a new block
     const bool nxt_cb_exists = CB + 1 < NCB || nx_exists;
-    auto wl = [&](int q) { return q >= 0 && q + 3 < S_tot ? 1 : 0; };  // a weight load was issued at step q
-    // VMEM operations issued after the last piece of the halo the next k-step reads (exact)
+    auto wl = [&](int q) { return q >= 0 ? 1 : 0; };  // a weight load is issued at every step q >= 0
+    // VMEM operations issued after the last piece of the halo the next k-step reads (exact);
+    // within a step the halo pieces (J 0, 4, 6, 8) precede the weight load
     int younger = 0;
-    if constexpr (J == 3) younger = wl(s - 3) + wl(s - 2) + wl(s - 1) + npw;
-    if constexpr (J == 5) younger = wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + npw;
-    if constexpr (J == 7) younger = wl(s - 2) + wl(s - 1) + (nxt_cb_exists ? npw : 0);
-    if constexpr (J == 8) younger = wl(s - 1);
+    if constexpr (J == 3) younger = wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + HPW;
+    if constexpr (J == 5) younger = wl(s - 5) + wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + HPW;
+    if constexpr (J == 7) younger = wl(s - 3) + wl(s - 2) + wl(s - 1) + HPW;
+    if constexpr (J == 8) younger = wl(s - 2) + wl(s - 1);
     if constexpr (BOUNDARY) wait_vm_n(s + 1 < S_tot ? younger : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -322,7 +339,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
     constexpr bool FIRST = CB == 0 && J == 0 && decltype(first)::value;
     constexpr int PAR = decltype(par)::value;
-    if (s + 3 < S_tot) w_load(wreg[PAR ^ 1]);
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<J>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<J>{}, xc, wc1, H1);
@@ -330,8 +346,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
     read_one(IC<2>{}, IC<1>{}, IC<J>{}, xc, wc1, H1);
     read_one(IC<3>{}, IC<1>{}, IC<J>{}, xc, wc1, H1);
-    if (s + 2 < S_tot)
-      *reinterpret_cast<u32x4*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = wreg[PAR];
+    *reinterpret_cast<u32x4*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = wreg[(PAR + 2) & 3];
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<2>{}, IC<FIRST>{}, H0);
     read_one(IC<4>{}, IC<1>{}, IC<J>{}, xc, wc1, H1);
@@ -345,7 +360,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         if constexpr (CB + 1 < NCB) {
           issue_block(cur_fr, cur_y0, cur_x0, CB + 1, J == 6 ? 0 : 1, tbuf);
         } else {
-          if (nx_exists) issue_block(nx_fr, nx_y0, nx_x0, 0, J == 6 ? 0 : 1, tbuf);
+          issue_block(nx_fr, nx_y0, nx_x0, 0, J == 6 ? 0 : 1, tbuf);  // (last tile: itself, into a free buffer)
         }
       }
     }
@@ -355,6 +370,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<0>{}, IC<false>{}, H1);
+    w_load(wreg[(PAR + 1) & 3]);  // k-step s+5 (past the end: re-reads the panel; away from the barrier)
     if (do_r) {
       read_one(IC<0>{}, IC<0>{}, IC<NJ>{}, xn, wn0, H0);
       read_one(IC<1>{}, IC<0>{}, IC<NJ>{}, xn, wn0, H0);
@@ -380,22 +396,23 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 
   auto cblock = [&](auto cbc) __attribute__((always_inline)) {
     constexpr int CB = decltype(cbc)::value;
-    constexpr int P0 = (CB * 9) & 1;
-    step(cbc, IC<0>{}, IC<1>{}, IC<P0>{});
-    step(cbc, IC<1>{}, IC<0>{}, IC<P0 ^ 1>{});
-    step(cbc, IC<2>{}, IC<0>{}, IC<P0>{});
-    step(cbc, IC<3>{}, IC<0>{}, IC<P0 ^ 1>{});
-    step(cbc, IC<4>{}, IC<0>{}, IC<P0>{});
-    step(cbc, IC<5>{}, IC<0>{}, IC<P0 ^ 1>{});
-    step(cbc, IC<6>{}, IC<0>{}, IC<P0>{});
-    step(cbc, IC<7>{}, IC<0>{}, IC<P0 ^ 1>{});
-    step(cbc, IC<8>{}, IC<0>{}, IC<P0>{});
+    constexpr int P0 = CB * 9;  // k-step index within the tile (SPT % 4 == 0: the set is static)
+    step(cbc, IC<0>{}, IC<1>{}, IC<(P0 + 0) & 3>{});
+    step(cbc, IC<1>{}, IC<0>{}, IC<(P0 + 1) & 3>{});
+    step(cbc, IC<2>{}, IC<0>{}, IC<(P0 + 2) & 3>{});
+    step(cbc, IC<3>{}, IC<0>{}, IC<(P0 + 3) & 3>{});
+    step(cbc, IC<4>{}, IC<0>{}, IC<(P0 + 4) & 3>{});
+    step(cbc, IC<5>{}, IC<0>{}, IC<(P0 + 5) & 3>{});
+    step(cbc, IC<6>{}, IC<0>{}, IC<(P0 + 6) & 3>{});
+    step(cbc, IC<7>{}, IC<0>{}, IC<(P0 + 7) & 3>{});
+    step(cbc, IC<8>{}, IC<0>{}, IC<(P0 + 8) & 3>{});
   };
 
-  static_assert(NCB == 4, "tile body is unrolled for 4 channel blocks");
+  static_assert(NCB == 4 && SPT % 4 == 0, "tile body is unrolled for 4 channel blocks; 4 weight register sets");
   for (; tl < ntl;) {
     nx_exists = tl + 1 < ntl;
     if (nx_exists) tile_of(tl + 1, nx_fr, nx_y0, nx_x0);
+    else nx_fr = cur_fr, nx_y0 = cur_y0, nx_x0 = cur_x0;
     cblock(IC<0>{});
     cblock(IC<1>{});
     cblock(IC<2>{});

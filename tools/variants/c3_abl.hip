@@ -21,8 +21,10 @@
 //    buffer-OOB, so they read as zero with no per-lane branches) and the 9 taps read shifted
 //    windows of it at compile-time immediate ds_read offsets: 1.2x input traffic instead of 9x;
 //  * two halo buffers (the next channel block — or the next tile's first — streams in during
-//    taps 0..5 of the current one), a 5-slot weight ring (8 KiB per k-step, LDS-DMA from a
-//    k-step-major, pre-swizzled copy of the weights: each 1 KiB piece is contiguous), one raw
+//    taps 0..5 of the current one), a 3-slot weight ring (8 KiB per k-step from a k-step-major,
+//    pre-swizzled copy of the weights: each wave's 1 KiB piece is contiguous; loaded into
+//    registers five k-steps ahead (4 register sets) and written with ds_write_b128 two steps
+//    before use — deep enough for the few-tile layers that stream weights from HBM), one raw
 //    s_barrier per k-step with an exact counted vmcnt;
 //  * fragment reads run one 16-deep sub-step ahead of the MFMAs (6 ds_read_b128 per half
 //    k-step, two register sets) and the k-step's LDS-DMA pieces are issued between MFMA pairs;
@@ -30,11 +32,19 @@
 //    pack, v_permlane32_swap pairs into 16-byte stores), so the next tile's prefetched halo and
 //    weights are already in flight while it runs: no per-tile prologue, no LDS staging.
 // LDS: halo 2 x 48 KiB (pixel pitch 80 B = 64 B of channels + 16 B pad: conflict-free
-// ds_read_b128 for 32-pixel rows), weight ring 5 x 8 KiB (XOR-swizzled 64 B rows), bias.
+// ds_read_b128 for 32-pixel rows), weight ring 3 x 8 KiB (XOR-swizzled 64 B rows), bias.
 #include "conv_common.h"
 
 #include <type_traits>
 
+// Ablation variant (timing only, wrong results): C3_ABL bits 1 halo DMA, 2 weight staging,
+// 4 fragment reads, 8 per-step barrier, 16 epilogue, 32 weight ds_write only, 64 ds_write of a
+// constant, 128 (valid) ds_write after the mid-step fragment wait, 256 per-block rotated weight
+// k-steps (L2 hot-spot test); 512 / 1024 (valid) weight load in the second half of the k-step;
+// 2048 (valid) weight load and halo piece both in the second half
+#ifndef C3_ABL
+#define C3_ABL 0
+#endif
 namespace tv {
 namespace c3 {
 
@@ -42,7 +52,8 @@ constexpr int NT = 512, NW = 8, BN = 128, P = 512;
 constexpr int WP = P / NW;                    // pixels per wave = 64 (two 32-pixel fragments)
 constexpr int CBK = 32;                       // channels per k-step
 constexpr int NCB = 128 / CBK;                // channel blocks per tile (C == 128)
-constexpr int SPT = 9 * NCB;                  // k-steps per tile
+template <int RES>
+constexpr int spt() { return (9 + RES) * NCB; }
 constexpr int PITCH = 80;                     // halo pixel pitch (bytes)
 constexpr int HPIX = 612;                     // (16+2)x(32+2) = (32+2)x(16+2) halo pixels
 constexpr int HPIECES = 48;                   // ceil(612 * 5 / 64) LDS-DMA pieces of 1 KiB
@@ -50,12 +61,16 @@ constexpr int HBUF = HPIECES * 1024;          // one halo buffer
 constexpr int HPW = HPIECES / NW;             // halo pieces per wave per channel block = 6
 constexpr int HTAPS = HPW;                    // one halo piece per k-step, taps 0..5
 constexpr int WSLOT = BN * 64;                // weights of one k-step: 128 rows x 64 B
-constexpr int D = 4;                          // weight prefetch distance (k-steps)
-constexpr int RING = D + 1;                   // weight ring slots: a k-step's slot is re-filled
-                                              // only after every wave has finished reading it
+constexpr int RING = 3;                       // weight ring slots (register-staged: k-step q is
+                                              // loaded at step q-3, written to LDS at step q-2)
 constexpr int OFF_W = 2 * HBUF;
 constexpr int OFF_B = OFF_W + RING * WSLOT;
-constexpr int LDS = OFF_B + kConv3MaxN * 4;
+constexpr int OFF_R = OFF_B + kConv3MaxN * 4;  // RES: one channel block of the residual input
+constexpr int RBUF = 512 * 64;                  // 512 pixels x 32 channels (XOR-swizzled 16 B chunks)
+constexpr int RPW = RBUF / 1024 / NW;           // residual pieces per wave per channel block = 4
+template <int RES>
+constexpr int lds_bytes() { return OFF_R + (RES ? RBUF : 0); }
+static_assert(lds_bytes<1>() <= 160 * 1024, "LDS budget");
 static_assert(WSLOT / 1024 == NW, "one weight piece per wave per k-step");
 static_assert(HPIECES * 64 >= HPIX * 5, "halo pieces");
 
@@ -89,7 +104,8 @@ __device__ __forceinline__ void wait_vm_n(int n) {
     case 2: wait_vm<2>(); break;
     case 3: wait_vm<3>(); break;
     case 4: wait_vm<4>(); break;
-    default: wait_vm<5>(); break;
+    case 5: wait_vm<5>(); break;
+    default: wait_vm<6>(); break;
   }
 }
 
@@ -119,9 +135,10 @@ __device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh
   gstore16(dst + 8 * lh, make_uint4(r0[0], r1[0], r0[1], r1[1]));
 }
 
-template <typename T, typename OutT, int TW, int ACT>
+template <typename T, typename OutT, int TW, int ACT, int EPI, int RES>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
+  constexpr int SPTK = spt<RES>();  // k-steps per tile
   constexpr int TH = P / TW;
   constexpr int RS = TW + 2;                               // halo row stride (pixels)
   constexpr int FOFF = (TW == 32 ? 1 : 2) * RS * PITCH;    // next 32-pixel fragment
@@ -161,7 +178,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
   if (ntl == 0) return;
-  const int S_tot = ntl * SPT;
+  const int S_tot = ntl * SPTK;
 
   // bias of every output channel into LDS (read in the epilogues)
   float* lbias = reinterpret_cast<float*>(smem + OFF_B);
@@ -223,17 +240,54 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
                         cb * CBK * (int)sizeof(T), 0, 0);
   };
 
+  // ---- RES: the ResidualBlock's 1x1 conv_residual (dla.py:32-37) as a 10th k-step per
+  // channel block. Its input x (second segment, stride rstr) for the tile's 512 output pixels
+  // moves into one 32 KiB LDS buffer per channel block: chunk L = piece*64 + lane holds pixel
+  // q = L/4, source chunk (L % 4) ^ ((q >> 2) & 3) (conflict-free fragment reads). One buffer
+  // resource per frame keeps offsets below 2^31.
+  [[maybe_unused]] unsigned rgeo[RPW];
+  [[maybe_unused]] const ConvSegment& sr = p.seg[RES ? 1 : 0];
+  [[maybe_unused]] const unsigned rpix_bytes = (unsigned)sr.ldc * (unsigned)sizeof(T);
+  if constexpr (RES) {
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int L = (wave * RPW + i) * 64 + lane;
+      const int q = L >> 2;
+      rgeo[i] = (unsigned)((q << 2) | ((L & 3) ^ ((q >> 2) & 3)));
+    }
+  }
+  auto res_piece = [&](int i, int fr, int y0, int x0, int cb) __attribute__((always_inline)) {
+    const unsigned long long fb = (unsigned long long)sr.H * sr.W * rpix_bytes;
+    const unsigned long long a = (unsigned long long)sr.src + (unsigned long long)fr * fb;
+    i32x4 rs;
+    rs.x = (int)(unsigned)a;
+    rs.y = (int)(unsigned)(a >> 32);
+    rs.z = (int)(unsigned)fb;
+    rs.w = 0x00020000;
+    const int q = (int)(rgeo[i] >> 2), c = (int)(rgeo[i] & 3);
+    const int y = y0 + q / TW, x = x0 + q % TW;
+    const bool ok = y < H && x < W;
+    const unsigned off = ok ? ((unsigned)(y * sr.stride) * (unsigned)sr.W + (unsigned)(x * sr.stride)) * rpix_bytes +
+                                  (unsigned)c * 16u
+                            : 0x80000000u;
+    raw_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + OFF_R + (wave * RPW + i) * 1024), 16,
+                        (int)off, cb * CBK * (int)sizeof(T), 0, 0);
+  };
+
   // ---- weight issue cursor: k-step counter and the global k-step index of the next piece
-  int wc_q = 0, wc_idx = 0, wc_in = 0, wc_nt = 0;
+  int wc_idx = 0, wc_in = 0, wc_nt = 0;
   {
     int a, b_, c_;
     tile_of(0, a, b_, c_, wc_nt);
   }
-  auto w_piece = [&]() __attribute__((always_inline)) {
-    const char* src = wts + (size_t)(wc_nt * SPT + wc_in) * WSLOT;
-    dma16(src, lds + OFF_W + (wc_q % RING) * WSLOT + wave * 1024);
-    ++wc_q;
-    if (++wc_in == SPT) {
+  // register-staged weights: one 16-byte global load per lane per k-step, written to the
+  // ring slot with ds_write_b128 one step later (instead of an LDS-DMA piece per k-step)
+  u32x4 wreg[4];  // k-step q's weights are loaded at step q-5 into set q % 4
+  auto w_load = [&](u32x4& dst) __attribute__((always_inline)) {
+    const char* src = (C3_ABL & 256) ? wts + (size_t)(wc_nt * SPTK + (wc_in + 9 * (bid >> 3)) % SPTK) * WSLOT
+                                     : wts + (size_t)(wc_nt * SPTK + wc_in) * WSLOT;
+    dst = *(g_cu32x4*)src;
+    if (++wc_in == SPTK) {
       wc_in = 0;
       if (++wc_idx < ntl) {
         int a, b_, c_;
@@ -255,16 +309,28 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   for (int j = 0; j < 2; ++j)
     wa[j] = lds0 + OFF_W + (unsigned)(l32 * 64 + (((2 * j + lh) ^ ((l32 >> 2) & 3)) << 4));
 
-  bool abl_done = false;
-  // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]
+  // RES: fragment base of pixel q0 = WP*wave + l32 in the residual buffer, per sub-step J
+  // (fragment f = 1 is q0 + 32: +2 KiB, same swizzle)
+  [[maybe_unused]] unsigned rxa[2];
+  if constexpr (RES) {
+    const int q0 = WP * wave + l32;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) rxa[j] = lds0 + OFF_R + (unsigned)(q0 * 64 + (((2 * j + lh) ^ ((q0 >> 2) & 3)) << 4));
+  }
+
+  // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]; TAP 9 = residual k-step
+  bool abl_rd = false;
   auto read_one = [&](auto r, auto j, auto tap, unsigned xb, unsigned wb, Half& F) __attribute__((always_inline)) {
     constexpr int R = decltype(r)::value, J = decltype(j)::value, TAP = decltype(tap)::value;
-#ifdef ABL_NOREAD
-    if (abl_done) return;
-#endif
-    constexpr int TOFF = ((TAP / 3) * RS + (TAP % 3)) * PITCH;
-    if constexpr (R < 2) F.x[R] = ds_read16<TOFF + 32 * J + R * FOFF>(xb);
-    else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
+    if ((C3_ABL & 4) && abl_rd) return;
+    if constexpr (TAP == 9) {
+      if constexpr (R < 2) F.x[R] = ds_read16<R * 2048>(rxa[J]);
+      else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
+    } else {
+      constexpr int TOFF = ((TAP / 3) * RS + (TAP % 3)) * PITCH;
+      if constexpr (R < 2) F.x[R] = ds_read16<TOFF + 32 * J + R * FOFF>(xb);
+      else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
+    }
   };
 
   f32x16 acc[2][4];  // [pixel fragment f][channel fragment i]; first written by a tile's first k-step
@@ -291,6 +357,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       const bool ok = y < H && x < W;
       OutT* dst = reinterpret_cast<OutT*>(out_ptr) +
                   ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.out_ldc + p.out_coff + n0;
+      [[maybe_unused]] f32x16 hacc = f32x16{};  // EPI 1: the 1x1 heads' partial sums of this pixel
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -308,15 +375,42 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
               v[gg][e] = t;
             }
           }
-          const int ch = n0 + 32 * i + 16 * m;
-          if (ok && ch < p.N) store_out<OutT>(dst + 32 * i + 16 * m, v, lh);
+          if constexpr (EPI == 0) {
+            const int ch = n0 + 32 * i + 16 * m;
+            if (ok && ch < p.N) store_out<OutT>(dst + 32 * i + 16 * m, v, lh);
+          } else {
+            // the 8 hidden channels 32i+16m+8lh.. of this pixel, rounded to T exactly as the
+            // unfused path stores them, are the MFMA B operand of k-step 2i+m of the 1x1
+            const unsigned a0 = pack2<T>(v[0][0], v[0][1]), a1 = pack2<T>(v[0][2], v[0][3]);
+            const unsigned b0 = pack2<T>(v[1][0], v[1][1]), b1 = pack2<T>(v[1][2], v[1][3]);
+            const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            const uint4 hv = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+            const uint4 hwf = gload16(reinterpret_cast<const char*>(p.head_w) +
+                                      ((size_t)(nt * 8 + 2 * i + m) * 64 + lane) * 16);
+            Mfma<T>::run(hwf, hv, hacc);
+          }
           __builtin_amdgcn_sched_barrier(0);  // bound the live set: one 8-channel group at a time
         }
+      }
+      if constexpr (EPI == 1) {
+        // rows r = 8G + 4lh + e of the 1x1 result: output column head_row0[nt] + r of pixel (y, x)
+        const int nr = p.head_nrows[nt];
+        float* hd = reinterpret_cast<float*>(out_ptr) + ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.head_ldc +
+                    p.head_row0[nt];
+        const float* hb = p.head_b + nt * 32;
+#pragma unroll
+        for (int G = 0; G < 4; ++G)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 8 * G + 4 * lh + e;
+            if (ok && r < nr) unsafeAtomicAdd(hd + r, hacc[4 * G + e] + hb[r]);
+          }
       }
     }
   };
 
-  // ---- prologue: halo of (tile 0, block 0), weights of k-steps 0..D-1
+  // ---- prologue: halo of (tile 0, block 0), weights of k-steps 0..2
   int cur_fr, cur_y0, cur_x0, cur_nt;
   tile_of(0, cur_fr, cur_y0, cur_x0, cur_nt);
   halo_offsets(cur_fr, cur_y0, cur_x0);
@@ -326,9 +420,23 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   halo_piece(IC<3>{}, 0, 0);
   halo_piece(IC<4>{}, 0, 0);
   halo_piece(IC<5>{}, 0, 0);
-  for (int q = 0; q < D; ++q)
-    if (q < S_tot) w_piece();
-  wait_vm_n(S_tot - 1 < D - 1 ? S_tot - 1 : D - 1);  // weights 1..D-1 may stay in flight
+  __builtin_amdgcn_sched_barrier(0);  // the counted wait below needs the halo issued first
+  // weights: k-steps 0, 1 into ring slots 0, 1; k-steps 2, 3, 4 in flight in sets 2, 3, 0
+  // (S_tot >= SPTK > 5). Every VMEM operation of the main loop is issued unconditionally —
+  // past the end of the list the weight loads re-read the last tile's k-steps and the halo
+  // pieces reload the current tile into the idle buffer — so that the compiler's own vmcnt
+  // for each weight ds_write is exact: a conditional load makes it fall back to vmcnt(0),
+  // which drains the halo pieces and weight loads issued since (measured: ~20% of the layer).
+  w_load(wreg[0]);
+  w_load(wreg[1]);
+  *reinterpret_cast<u32x4*>(smem + OFF_W + wave * 1024 + lane * 16) = wreg[0];
+  *reinterpret_cast<u32x4*>(smem + OFF_W + WSLOT + wave * 1024 + lane * 16) = wreg[1];
+  w_load(wreg[2]);
+  w_load(wreg[3]);
+  w_load(wreg[0]);
+  // the halo (issued first) landed; the weights of k-steps 2..4 may stay in flight
+  wait_vm<3>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
@@ -340,7 +448,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   if (p.stamps) st1 = __builtin_amdgcn_s_memtime();
-  abl_done = true;
+  abl_rd = true;
 
   int s = 0;   // global k-step
   int tl = 0;  // tile index within this block's list
@@ -353,40 +461,42 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // half (8 MFMAs on H1) the reads of the NEXT k-step's sub-step-0 fragments into H0. The
   // k-step's LDS-DMA pieces (1 weight, <= 1 halo) are issued between MFMA pairs.
   // Halo buffer of channel block cb is cb & 1 (NCB is even, so parity is per-tile fixed).
-  auto step = [&](auto tap, auto first) __attribute__((always_inline)) {
+  auto step = [&](auto tap, auto first, auto par) __attribute__((always_inline)) {
     constexpr int TAP = decltype(tap)::value;
-    // LDS-DMA instructions allowed in flight: those issued after weights(s+1) — weight pieces
-    // of s+2, s+3 (issued at steps s-2, s-1) and halo pieces at steps s-3..s-1 of this channel
-    // block with tap < HTAPS — except at tap 8, where the next k-step reads the NEXT channel
-    // block's halo: then every halo piece must have landed (only the 2 weight pieces issued
-    // after the last one, at taps 6 and 7, may stay in flight)
-    constexpr int hsteps = TAP == 8 ? 0
-                                    : (TAP >= 1 ? 1 : 0) * (TAP - 1 < HTAPS) + (TAP >= 2 ? 1 : 0) * (TAP - 2 < HTAPS) +
-                                          (TAP >= 3 ? 1 : 0) * (TAP - 3 < HTAPS);
-    static_assert(HTAPS <= 6, "weights issued after the last halo piece must cover the tap-8 count");
-    const int younger = (s + 2 < S_tot) + (s + 3 < S_tot) + (nxt_exists ? hsteps : 0);
+    // Weights of k-step s+1 were written to LDS at step s-1 (lgkmcnt + barrier below); halo and
+    // residual data arrive by LDS-DMA and are waited for with an exact vmcnt: the count of
+    // vector-memory operations issued after the last piece the next k-step reads. A weight load
+    // is issued at every step q >= 0; within a step the order is weight load, halo piece
+    // (taps 0..5, next channel block), residual piece (RES, taps 1..4, this channel block).
+    //  * tap 8 without RES / residual step (tap 9): the next k-step reads the NEXT channel
+    //    block's halo (last piece at tap 5): younger = the weight loads of taps 6, 7 (and 8);
+    //  * tap 8 with RES: the residual step reads this block's residual input (last piece at
+    //    tap 4): younger = weight loads of taps 5, 6, 7 + the tap-5 halo piece.
+    static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
+    auto wl = [&](int q) { return q >= 0 ? 1 : 0; };
     unsigned long long tw0 = 0;
     if (p.stamps) tw0 = __builtin_amdgcn_s_memtime();
-    wait_vm_n(s + 1 < S_tot ? younger : 0);
+    constexpr int WLATE = (C3_ABL & (512 | 1024)) ? 1 : 0;  // weight load after the halo/residual pieces
+    constexpr int HLATE = (C3_ABL & 2048) ? 1 : 0;  // w_load after pair 0 of H1, halo after pair 2 of H1
+    if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? 2 + WLATE : 0);
+    if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? (HLATE ? 6 : 4 + WLATE) : 0);
+    if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? 3 + WLATE : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifndef ABL_NOBAR
-    __builtin_amdgcn_s_barrier();
-#endif
+    if (!(C3_ABL & 8)) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (p.stamps) stall += __builtin_amdgcn_s_memtime() - tw0;
 
-    constexpr int NTAP = TAP == 8 ? 0 : TAP + 1;
+    constexpr int NTAP = TAP == 8 ? (RES ? 9 : 0) : TAP == 9 ? 0 : TAP + 1;
     const bool do_r = s + 1 < S_tot;
     const int hbuf = (cb + 1) & 1;
-    const unsigned xc = xa + (cb & 1) * HBUF;                         // this k-step's halo
-    const unsigned xn = xa + (TAP == 8 ? hbuf : (cb & 1)) * HBUF;     // next k-step's halo
+    const unsigned xc = xa + (cb & 1) * HBUF;                                  // this k-step's halo
+    const unsigned xn = xa + (NTAP == 0 ? hbuf : (cb & 1)) * HBUF;             // next k-step's halo
     const unsigned wc1 = wa[1] + (unsigned)((s % RING) * WSLOT);
     const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
-#ifndef ABL_NODMA
-    if (s + D < S_tot) w_piece();
-#endif
+    constexpr int PAR = decltype(par)::value;  // s % 4 (36 or 40 k-steps per tile: static)
+    if (!(C3_ABL & (2 | 512 | 1024 | 2048))) w_load(wreg[(PAR + 1) & 3]);   // k-step s+5 (that set's k-step s+1 is in LDS)
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
@@ -394,6 +504,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
     read_one(IC<2>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<3>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+    // k-step s+2 (loaded at step s-3) into its ring slot: it last held k-step s-1, read
+    // completely before this step's barrier (past the end: an unread slot)
+    if (!(C3_ABL & (34 | 128))) *reinterpret_cast<u32x4*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = (C3_ABL & 64) ? u32x4{1u, 2u, 3u, 4u} : wreg[(PAR + 2) & 3];
     if constexpr (TAP == 0) {
       if (nxt_exists && nxt_newtile) {
         int fr, y0, x0, nt;
@@ -405,28 +518,31 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     mfma_pair(IC<2>{}, IC<FIRST>{}, H0);
     read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-#ifndef ABL_NODMA
     if constexpr (TAP < HTAPS)
-      if (nxt_exists) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);
-#endif
+      if (!(C3_ABL & (1 | 2048))) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);  // (no next block: the idle buffer)
+    if constexpr (RES && TAP >= 1 && TAP <= RPW) res_piece(TAP - 1, cur_fr, cur_y0, cur_x0, cb);
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<3>{}, IC<FIRST>{}, H0);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<0>{}, IC<false>{}, H1);
+    if (C3_ABL & (1024 | 2048)) w_load(wreg[(PAR + 1) & 3]);
+    if (C3_ABL & 128) *reinterpret_cast<u32x4*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = wreg[(PAR + 2) & 3];
     if (do_r) {
       read_one(IC<0>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<1>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<1>{}, IC<false>{}, H1);
+    if (C3_ABL & 512) w_load(wreg[(PAR + 1) & 3]);
     if (do_r) {
       read_one(IC<2>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<3>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
     }
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<2>{}, IC<false>{}, H1);
+    if constexpr ((C3_ABL & 2048) && TAP < HTAPS) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);
     if (do_r) {
       read_one(IC<4>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<5>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
@@ -442,20 +558,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     cb = CB;
     nxt_newtile = CB + 1 == NCB;
     nxt_exists = !nxt_newtile || tl + 1 < ntl;
-    step(IC<0>{}, IC<CB == 0>{});
-    step(IC<1>{}, IC<false>{});
-    step(IC<2>{}, IC<false>{});
-    step(IC<3>{}, IC<false>{});
-    step(IC<4>{}, IC<false>{});
-    step(IC<5>{}, IC<false>{});
-    step(IC<6>{}, IC<false>{});
-    step(IC<7>{}, IC<false>{});
-    step(IC<8>{}, IC<false>{});
+    constexpr int P0 = CB * (9 + RES);  // k-step index of the block's tap 0 within the tile
+    step(IC<0>{}, IC<CB == 0>{}, IC<(P0 + 0) & 3>{});
+    step(IC<1>{}, IC<false>{}, IC<(P0 + 1) & 3>{});
+    step(IC<2>{}, IC<false>{}, IC<(P0 + 2) & 3>{});
+    step(IC<3>{}, IC<false>{}, IC<(P0 + 3) & 3>{});
+    step(IC<4>{}, IC<false>{}, IC<(P0 + 4) & 3>{});
+    step(IC<5>{}, IC<false>{}, IC<(P0 + 5) & 3>{});
+    step(IC<6>{}, IC<false>{}, IC<(P0 + 6) & 3>{});
+    step(IC<7>{}, IC<false>{}, IC<(P0 + 7) & 3>{});
+    step(IC<8>{}, IC<false>{}, IC<(P0 + 8) & 3>{});
+    if constexpr (RES) step(IC<9>{}, IC<false>{}, IC<(P0 + 9) & 3>{});
   };
 
   // 4 channel blocks per tile, fully unrolled (36 k-steps of straight-line code): the
   // accumulators keep one register assignment through the whole tile
-  static_assert(NCB == 4, "tile body is unrolled for 4 channel blocks");
+  static_assert(NCB == 4 && spt<0>() % 4 == 0 && spt<1>() % 4 == 0, "tile body: 4 channel blocks, k-steps per tile a multiple of the 4 weight register sets");
   for (; tl < ntl;) {
     cblock(IC<0>{});
     cblock(IC<1>{});
@@ -463,7 +581,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     cblock(IC<3>{});
     unsigned long long te0 = 0;
     if (p.stamps) te0 = __builtin_amdgcn_s_memtime();
-    epilogue(cur_fr, cur_y0, cur_x0, cur_nt);
+    if (!(C3_ABL & 16)) epilogue(cur_fr, cur_y0, cur_x0, cur_nt);
+    else if (tid == 0 && p.N < 0) {  // keep the accumulators live
+      float t = 0.0f;
+#pragma unroll
+      for (int f = 0; f < 2; ++f)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) t += acc[f][i][e];
+      *(float*)out_ptr = t;
+    }
     if (p.stamps) epi += __builtin_amdgcn_s_memtime() - te0;
     ++tl;
     if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
@@ -478,32 +606,35 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 }
 
-// [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q = cb*9 + tap][128 rows][4 x 16 B],
-// slot s of row r holding chunk s ^ ((r >> 2) & 3) of the k-step
-__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, uint4* __restrict__ out) {
-  const int n = ntiles * SPT * BN * 4;
+// [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q][128 rows][4 x 16 B], q = cb*9 + tap
+// (res: q = cb*10 + j, j = 9 the residual segment's channel block cb at K offset 9*128), slot s
+// of row r holding chunk s ^ ((r >> 2) & 3) of the k-step
+__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, int res, uint4* __restrict__ out) {
+  const int sp = res ? spt<1>() : spt<0>();
+  const int n = ntiles * sp * BN * 4;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
-    const int slot = o & 3, row = (o >> 2) & (BN - 1), q = (o >> 9) % SPT, nt = (o >> 9) / SPT;
+    const int slot = o & 3, row = (o >> 2) & (BN - 1), q = (o >> 9) % sp, nt = (o >> 9) / sp;
     const int chunk = slot ^ ((row >> 2) & 3);
-    const int cb = q / 9, tap = q - cb * 9;
-    const int k16 = (tap * 128 + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements)
+    const int cb = q / (9 + res), tap = q - cb * (9 + res);
+    const int k16 = (tap * 128 + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements); tap 9 = residual
     out[o] = w[(size_t)(nt * BN + row) * kpad16 + k16];
   }
 }
 
-template <typename T, int TW, int ACT>
+template <typename T, int TW, int ACT, int EPI = 0, int RES = 0>
 static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
-  auto k = conv3x3<T, T, TW, ACT>;
+  auto k = conv3x3<T, T, TW, ACT, EPI, RES>;
+  constexpr int lds = lds_bytes<RES>();
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) {
       set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
       return 3;
     }
     attr = true;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), LDS, s, dp, out);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, out);
   TV_HIP(hipGetLastError());
   return 0;
 }
@@ -515,24 +646,46 @@ int conv3x3_tiles(int B, int H, int W, int tw) {
   return B * ((H + th - 1) / th) * ((W + tw - 1) / tw);
 }
 
-size_t conv3x3_weight_bytes(int ntiles) { return (size_t)ntiles * c3::SPT * c3::WSLOT; }
+size_t conv3x3_weight_bytes(int ntiles, int res) {
+  return (size_t)ntiles * (res ? c3::spt<1>() : c3::spt<0>()) * c3::WSLOT;
+}
 
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, void* out, hipStream_t s) {
-  if ((Kpad * esz) % 16 || Kpad < 9 * 128) {
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, void* out, hipStream_t s) {
+  if ((Kpad * esz) % 16 || Kpad < (res ? 10 : 9) * 128) {
     set_error("conv3x3_repack: bad Kpad");
     return 1;
   }
-  hipLaunchKernelGGL(c3::repack_weights, dim3(256), dim3(256), 0, s, (const uint4*)w, Kpad * esz / 16, ntiles,
+  hipLaunchKernelGGL(c3::repack_weights, dim3(256), dim3(256), 0, s, (const uint4*)w, Kpad * esz / 16, ntiles, res,
                      (uint4*)out);
   TV_HIP(hipGetLastError());
   return 0;
 }
 
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s) {
+                   hipStream_t s, int epi, int res) {
   using namespace c3;
   if (p.act < 0 || p.act > 2) {
     set_error("conv3x3: bad activation");
+    return 1;
+  }
+  if (res) {  // ResidualBlock conv2 + conv_residual: ReLU, plain stores
+    if (p.act != 1 || epi != 0 || p.nseg != 2 || p.ntiles != 1) {
+      set_error("conv3x3: residual k-steps need ReLU, one channel tile and two segments");
+      return 1;
+    }
+    if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 1, 0, 1>(p, dp, out, grid, s) : launch_t<_Float16, 16, 1, 0, 1>(p, dp, out, grid, s);
+    if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 1, 0, 1>(p, dp, out, grid, s) : launch_t<__bf16, 16, 1, 0, 1>(p, dp, out, grid, s);
+    set_error("conv3x3: fp16/bf16 only");
+    return 1;
+  }
+  if (epi == 1) {  // fused 1x1 heads: the stacked heads' LeakyReLU only
+    if (p.act != 2 || p.ntiles > 8) {
+      set_error("conv3x3: fused heads need LeakyReLU and <= 8 channel tiles");
+      return 1;
+    }
+    if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 2, 1>(p, dp, out, grid, s) : launch_t<_Float16, 16, 2, 1>(p, dp, out, grid, s);
+    if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 2, 1>(p, dp, out, grid, s) : launch_t<__bf16, 16, 2, 1>(p, dp, out, grid, s);
+    set_error("conv3x3: fp16/bf16 only");
     return 1;
   }
   using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);

@@ -70,6 +70,8 @@ typedef __attribute__((address_space(3))) char lds_char;
 typedef const __attribute__((address_space(1))) void gvoid;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
+__device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+__device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
 __device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
                                     int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
 
@@ -149,6 +151,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int tiles_f = ((H + TH - 1) / TH) * tiles_x;
   const int ntiles = p.ntiles;
   const int ntot = p.mtiles * ntiles;
+  [[maybe_unused]] const unsigned long long out_frame_bytes = (unsigned long long)H * W * p.out_ldc * sizeof(OutT);  // < 2^31 (host)
 
   // ---- this block's tiles: XCD-aware contiguous ranges
   const int G = gridDim.x, bid = blockIdx.x;
@@ -186,7 +189,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   // k-step-major weights: [ntile][k-step][128 rows][64 B], chunks pre-swizzled; one 1 KiB
   // piece per wave per k-step at ((ntile * SPT + q) * 8 + wave) KiB
-  const char* wts = reinterpret_cast<const char*>(p.weight) + wave * 1024 + lane * 16;
+  // (read through a buffer resource: one lane-offset VGPR, the k-step offset in an SGPR)
+  i32x4 wrsrc;
+  {
+    const unsigned long long a = (unsigned long long)p.weight;
+    wrsrc.x = (int)(unsigned)a;
+    wrsrc.y = (int)(unsigned)(a >> 32);
+    wrsrc.z = ntiles * SPTK * WSLOT;
+    wrsrc.w = 0x00020000;
+  }
+  const int wvoff = wave * 1024 + lane * 16;
 
   // ---- tile decode
   auto tile_of = [&](int idx, int& fr, int& y0, int& x0, int& nt) __attribute__((always_inline)) {
@@ -275,8 +287,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // ring slot with ds_write_b128 one step later (instead of an LDS-DMA piece per k-step)
   u32x4 wreg[4];  // k-step q's weights are loaded at step q-5 into set q % 4
   auto w_load = [&](u32x4& dst) __attribute__((always_inline)) {
-    const char* src = wts + (size_t)(wc_nt * SPTK + wc_in) * WSLOT;
-    dst = *(g_cu32x4*)src;
+    dst = raw_buffer_load_v4(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSLOT, 0);
     if (++wc_in == SPTK) {
       wc_in = 0;
       if (++wc_idx < ntl) {
@@ -343,8 +354,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       const int q = WP * wave + 32 * f + l32;
       const int y = y0 + q / TW, x = x0 + q % TW;
       const bool ok = y < H && x < W;
-      OutT* dst = reinterpret_cast<OutT*>(out_ptr) +
+      [[maybe_unused]] OutT* dst = reinterpret_cast<OutT*>(out_ptr) +
                   ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.out_ldc + p.out_coff + n0;
+      // EPI 0: stores through a per-frame buffer resource, every lane always issuing (invalid
+      // pixels / channels -> OOB offset, dropped): a fixed count of VMEM operations per tile
+      [[maybe_unused]] i32x4 orsrc;
+      [[maybe_unused]] unsigned obase = 0;
+      if constexpr (EPI == 0) {
+        const unsigned long long a = (unsigned long long)out_ptr + (unsigned long long)fr * out_frame_bytes;
+        orsrc.x = (int)(unsigned)a;
+        orsrc.y = (int)(unsigned)(a >> 32);
+        orsrc.z = (int)out_frame_bytes;
+        orsrc.w = 0x00020000;
+        obase = ok ? ((unsigned)(y * W + x) * (unsigned)p.out_ldc + (unsigned)(p.out_coff + n0 + 8 * lh)) * (unsigned)sizeof(OutT)
+                   : 0x80000000u;
+      }
       [[maybe_unused]] f32x16 hacc = f32x16{};  // EPI 1: the 1x1 heads' partial sums of this pixel
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -365,7 +389,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
           }
           if constexpr (EPI == 0) {
             const int ch = n0 + 32 * i + 16 * m;
-            if (ok && ch < p.N) store_out<OutT>(dst + 32 * i + 16 * m, v, lh);
+            const unsigned a0 = pack2<OutT>(v[0][0], v[0][1]), a1 = pack2<OutT>(v[0][2], v[0][3]);
+            const unsigned b0 = pack2<OutT>(v[1][0], v[1][1]), b1 = pack2<OutT>(v[1][2], v[1][3]);
+            const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            raw_buffer_store_v4(u32x4{r0[0], r1[0], r0[1], r1[1]}, orsrc,
+                                ch < p.N ? (int)(obase + (unsigned)((32 * i + 16 * m) * sizeof(OutT))) : (int)0x80000000u, 0, 0);
           } else {
             // the 8 hidden channels 32i+16m+8lh.. of this pixel, rounded to T exactly as the
             // unfused path stores them, are the MFMA B operand of k-step 2i+m of the 1x1
@@ -422,8 +451,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   w_load(wreg[2]);
   w_load(wreg[3]);
   w_load(wreg[0]);
-  // the halo (issued first) landed; the weights of k-steps 2..4 may stay in flight
-  wait_vm<3>();
+  if constexpr (EPI == 0) {
+    // as many (dropped: zero-size resource) stores as a tile epilogue issues, so that both paths
+    // into the tile loop carry the same VMEM sequence and the compiler's vmcnt for the first
+    // weight ds_writes of a tile leaves the previous tile's stores in flight
+    __builtin_amdgcn_sched_barrier(0);
+    i32x4 nul;
+    nul.x = (int)(unsigned)(unsigned long long)out_ptr;
+    nul.y = (int)(unsigned)((unsigned long long)out_ptr >> 32);
+    nul.z = 0;
+    nul.w = 0x00020000;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) raw_buffer_store_v4(u32x4{0u, 0u, 0u, 0u}, nul, k * 16, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // the halo (issued first) landed; the weights of k-steps 2..4 (and the dropped stores) may stay in flight
+  wait_vm<EPI == 0 ? 19 : 3>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);

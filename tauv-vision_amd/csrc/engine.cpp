@@ -471,7 +471,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const size_t src_bytes = (size_t)B * cs.H * cs.W * cs.ldc * esz;
       if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand && cs.C == 128 &&
           cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && src_bytes < (1ull << 31) &&
-          p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix) {
+          p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix &&
+          (size_t)cs.H * cs.W * p.out_ldc * esz < (1ull << 31)) {
         const int res = res2 ? 1 : 0;
         const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16), t32 = conv3x3_tiles(B, cs.H, cs.W, 32);
         const int tw = c3_tw_force ? c3_tw_force : t32 <= t16 ? 32 : 16;

@@ -41,7 +41,7 @@
 // 4 fragment reads, 8 per-step barrier, 16 epilogue, 32 weight ds_write only, 64 ds_write of a
 // constant, 128 (valid) ds_write after the mid-step fragment wait, 256 per-block rotated weight
 // k-steps (L2 hot-spot test); 512 / 1024 (valid) weight load in the second half of the k-step;
-// 2048 (valid) weight load and halo piece both in the second half
+// 2048 (valid) weight load and halo piece both in the second half; 4096 epilogue without stores
 #ifndef C3_ABL
 #define C3_ABL 0
 #endif
@@ -377,7 +377,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
           }
           if constexpr (EPI == 0) {
             const int ch = n0 + 32 * i + 16 * m;
-            if (ok && ch < p.N) store_out<OutT>(dst + 32 * i + 16 * m, v, lh);
+            if (ok && ch < ((C3_ABL & 4096) ? -p.N : p.N)) store_out<OutT>(dst + 32 * i + 16 * m, v, lh);
           } else {
             // the 8 hidden channels 32i+16m+8lh.. of this pixel, rounded to T exactly as the
             // unfused path stores them, are the MFMA B operand of k-step 2i+m of the 1x1

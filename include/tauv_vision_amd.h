@@ -96,9 +96,11 @@ const char* tv_engine_op_label(tv_engine* engine, int32_t index);
 /* Kernel family launch `index` uses at this batch size ("conv_pipe", "conv_igemm", "conv_halo",
  * "prep"); "" before the batch's workspace exists. Diagnostic (roofline attribution). */
 const char* tv_engine_op_kernel(tv_engine* engine, int32_t batch, int32_t index);
-/* How a forward of `batch` frames is launched: as *n_slices (1 or 2) concurrent slices of
- * slice_batch[0], slice_batch[1] frames (diagnostic: per-launch roofline attribution). */
-int tv_engine_slices(tv_engine* engine, int32_t batch, int32_t* n_slices, int32_t slice_batch[2]);
+/* How a forward of `batch` frames is launched: as *n_slices (1..TV_MAX_SLICES) concurrent slices
+ * of slice_batch[0..n_slices) frames, the rest of slice_batch zeroed (diagnostic: per-launch
+ * roofline attribution). */
+#define TV_MAX_SLICES 8
+int tv_engine_slices(tv_engine* engine, int32_t batch, int32_t* n_slices, int32_t slice_batch[TV_MAX_SLICES]);
 
 /* heatmap_nms(sigmoid?(heat), k) (decode.py:239-252) over any strided [B,C,H,W] fp32
  * view; `out` is dense [B,C,H,W]. k must be odd and >= 1 (else TV_EINVAL, like the

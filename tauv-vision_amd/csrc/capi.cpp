@@ -146,18 +146,12 @@ const char* tv_engine_op_label(tv_engine* e, int32_t i) {
   return e->e.plan.ops[i].label.c_str();
 }
 
-int tv_engine_slices(tv_engine* e, int32_t B, int32_t* n, int32_t sb[2]) {
+int tv_engine_slices(tv_engine* e, int32_t B, int32_t* n, int32_t sb[TV_MAX_SLICES]) {
   TV_GUARD({
     if (!e || !n || !sb || B < 1) { set_error("bad argument"); return TV_EINVAL; }
-    if (e->e.slices > 1 && B >= 2 * e->e.slice_min) {
-      *n = 2;
-      sb[0] = B / 2;
-      sb[1] = B - B / 2;
-    } else {
-      *n = 1;
-      sb[0] = B;
-      sb[1] = 0;
-    }
+    const std::vector<int> sz = e->e.slice_sizes(B);
+    *n = (int32_t)sz.size();
+    for (int k = 0; k < TV_MAX_SLICES; ++k) sb[k] = k < (int)sz.size() ? sz[k] : 0;
     return TV_OK;
   })
 }

@@ -316,7 +316,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto step = [&](auto cbc, auto jc, auto first, auto par) __attribute__((always_inline)) {
     constexpr int CB = decltype(cbc)::value, J = decltype(jc)::value;
     constexpr bool BOUNDARY = J == 3 || J == 5 || J == 7 || J == 8;  // the next k-step starts a new block
-    const bool nxt_cb_exists = CB + 1 < NCB || nx_exists;
     auto wl = [&](int q) { return q >= 0 ? 1 : 0; };  // a weight load is issued at every step q >= 0
     // VMEM operations issued after the last piece of the halo the next k-step reads (exact);
     // within a step the halo pieces (J 0, 4, 6, 8) precede the weight load

@@ -249,8 +249,14 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_SLICES")) slices = std::atoi(env);
-  if (const char* env = std::getenv("TV_STAGGER")) stagger = std::atoi(env);
+  if (const char* env = std::getenv("TV_SLICES")) slices = std::max(1, std::min(kMaxSlices, std::atoi(env)));
+  if (const char* env = std::getenv("TV_SLICE_SIZES")) {
+    for (const char* c = env; *c;) {
+      slice_sizes_env.push_back(std::atoi(c));
+      while (*c && *c != ',') ++c;
+      if (*c == ',') ++c;
+    }
+  }
   // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
   if (stem_mode && dtype != F32)
     for (size_t i = 0; i + 1 < plan.ops.size(); ++i)
@@ -286,8 +292,8 @@ Engine::~Engine() {
   }
   for (auto& kv : side) {
     if (kv.second.fork) (void)hipEventDestroy(kv.second.fork);
-    if (kv.second.join) (void)hipEventDestroy(kv.second.join);
-    if (kv.second.s) (void)hipStreamDestroy(kv.second.s);
+    for (hipEvent_t e : kv.second.join) (void)hipEventDestroy(e);
+    for (hipStream_t t : kv.second.s) (void)hipStreamDestroy(t);
   }
 }
 
@@ -680,18 +686,34 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   return TV_OK;
 }
 
-int Engine::get_side(hipStream_t s, SideStream** out) {
+int Engine::get_side(hipStream_t s, int n, SideStreams** out) {
   std::lock_guard<std::mutex> g(mu);
-  auto it = side.find((void*)s);
-  if (it == side.end()) {
-    SideStream ss;
-    TV_HIP(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
-    TV_HIP(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
-    TV_HIP(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
-    it = side.emplace((void*)s, ss).first;
+  SideStreams& ss = side[(void*)s];
+  if (!ss.fork) TV_HIP(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
+  while ((int)ss.s.size() < n) {
+    hipStream_t t;
+    hipEvent_t e;
+    TV_HIP(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+    TV_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ss.s.push_back(t);
+    ss.join.push_back(e);
   }
-  *out = &it->second;
+  *out = &ss;
   return TV_OK;
+}
+
+std::vector<int> Engine::slice_sizes(int B) const {
+  if (!slice_sizes_env.empty()) {
+    int sum = 0;
+    for (int v : slice_sizes_env) sum += v > 0 ? v : 1 << 30;
+    if (sum == B && (int)slice_sizes_env.size() <= kMaxSlices) return slice_sizes_env;
+  }
+  if (slices > 1 && B >= slices * slice_min) {
+    std::vector<int> sz(slices);
+    for (int k = 0; k < slices; ++k) sz[k] = B / slices + (k < B % slices ? 1 : 0);
+    return sz;
+  }
+  return {B};
 }
 
 int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStream_t s, size_t op0, size_t op1) {
@@ -707,17 +729,18 @@ int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStrea
 
 int Engine::prepare(int B, hipStream_t s) {
   TV_HIP(hipSetDevice(device));
-  if (slices > 1 && B >= 2 * slice_min) {
-    SideStream* ss = nullptr;
-    int rc = get_side(s, &ss);
-    if (rc) return rc;
-    Workspace* ws = nullptr;
-    rc = get_workspace(B / 2, s, &ws);
-    if (rc) return rc;
-    return get_workspace(B - B / 2, ss->s, &ws);
-  }
+  const std::vector<int> sz = slice_sizes(B);
   Workspace* ws = nullptr;
-  return get_workspace(B, s, &ws);
+  if (sz.size() > 1) {
+    SideStreams* ss = nullptr;
+    int rc = get_side(s, (int)sz.size() - 1, &ss);
+    if (rc) return rc;
+    for (size_t k = 1; k < sz.size(); ++k) {
+      rc = get_workspace(sz[k], ss->s[k - 1], &ws);
+      if (rc) return rc;
+    }
+  }
+  return get_workspace(sz[0], s, &ws);
 }
 
 int Engine::forward(const void* input, int input_u8, int B, float* out, hipStream_t s) {
@@ -730,29 +753,29 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
     return TV_EINVAL;
   }
   TV_HIP(hipSetDevice(device));
-  if (slices > 1 && B >= 2 * slice_min) {
-    // frames are independent (no cross-frame state): first half on `s`, second on the side
-    // stream, joined back into `s` (graph-capture safe: event fork / join)
-    SideStream* ss = nullptr;
-    int rc = get_side(s, &ss);
+  const std::vector<int> sz = slice_sizes(B);
+  if (sz.size() > 1) {
+    // frames are independent (no cross-frame state): slice 0 on `s`, the others on side
+    // streams forked from and joined back into `s` (graph-capture safe: event fork / join)
+    SideStreams* ss = nullptr;
+    int rc = get_side(s, (int)sz.size() - 1, &ss);
     if (rc) return rc;
-    const int B1 = B / 2;
     const size_t in_frame = input_u8 ? (size_t)desc.in_h * desc.in_w * 3 : (size_t)3 * desc.in_h * desc.in_w * 4;
     const size_t out_frame = (size_t)plan.out_h * plan.out_w * plan.out_cpad;
-    // optional staggered start (env TV_STAGGER = k): the side slice begins once the first has
-    // run its first k ops; measured no better than k = 0 (the persistent large-layer kernels
-    // occupy every CU, so the other slice's small launches cannot slip in beside them)
-    const size_t k = (size_t)stagger;
-    rc = run_all(input, input_u8, B1, out, s, 0, k);
-    if (rc) return rc;
     TV_HIP(hipEventRecord(ss->fork, s));
-    TV_HIP(hipStreamWaitEvent(ss->s, ss->fork, 0));
-    rc = run_all((const char*)input + B1 * in_frame, input_u8, B - B1, out + B1 * out_frame, ss->s);
+    size_t f0 = (size_t)sz[0];
+    for (size_t k = 1; k < sz.size(); ++k) {
+      TV_HIP(hipStreamWaitEvent(ss->s[k - 1], ss->fork, 0));
+      rc = run_all((const char*)input + f0 * in_frame, input_u8, sz[k], out + f0 * out_frame, ss->s[k - 1]);
+      if (rc) return rc;
+      f0 += (size_t)sz[k];
+    }
+    rc = run_all(input, input_u8, sz[0], out, s);
     if (rc) return rc;
-    rc = run_all(input, input_u8, B1, out, s, k);
-    if (rc) return rc;
-    TV_HIP(hipEventRecord(ss->join, ss->s));
-    TV_HIP(hipStreamWaitEvent(s, ss->join, 0));
+    for (size_t k = 1; k < sz.size(); ++k) {
+      TV_HIP(hipEventRecord(ss->join[k - 1], ss->s[k - 1]));
+      TV_HIP(hipStreamWaitEvent(s, ss->join[k - 1], 0));
+    }
     return TV_OK;
   }
   return run_all(input, input_u8, B, out, s);

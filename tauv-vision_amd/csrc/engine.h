@@ -66,17 +66,21 @@ struct Engine {
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1
   int halo_mode = 0;           // 1 enables the halo-tile 3x3 kernel, 2 forces it (env TV_CONV_HALO)
-  // concurrent slices: a batch of >= 2 * slice_min frames runs as two halves on the caller's
-  // stream and a side stream (fork / join events), so one half's latency-bound small layers
-  // overlap the other half's large ones (env TV_SLICES=1 off)
+  // concurrent slices: a batch of >= slices * slice_min frames runs as `slices` near-equal parts,
+  // the first on the caller's stream and the others on side streams (fork / join events), so one
+  // slice's latency-bound small layers and grid tails overlap another's large layers
+  // (env TV_SLICES: count, 1 = off; TV_SLICE_SIZES=a,b,...: explicit sizes for experiments)
+  static constexpr int kMaxSlices = 8;  // == TV_MAX_SLICES (include/tauv_vision_amd.h)
   int slices = 2;
   int slice_min = 8;
-  int stagger = 0;   // the side slice starts after this many ops of the first (env TV_STAGGER)
-  struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+  std::vector<int> slice_sizes_env;
+  std::vector<int> slice_sizes(int B) const;
+  struct SideStreams {
+    std::vector<hipStream_t> s;
+    hipEvent_t fork = nullptr;
+    std::vector<hipEvent_t> join;
   };
-  std::map<void*, SideStream> side;  // per caller stream
+  std::map<void*, SideStreams> side;  // per caller stream
   std::mutex mu;
   std::map<std::pair<void*, int>, Workspace*> workspaces;
   std::unordered_map<std::string, std::pair<const float*, int64_t>> host_w;  // during create only
@@ -98,7 +102,7 @@ struct Engine {
   int run_op(size_t i, Workspace* ws, const void* input, int input_u8, float* out, hipStream_t s);
   int run_all(const void* input, int input_u8, int B, float* out, hipStream_t s, size_t op0 = 0,
               size_t op1 = (size_t)-1);
-  int get_side(hipStream_t s, SideStream** out);
+  int get_side(hipStream_t s, int n, SideStreams** out);
 };
 
 }  // namespace tv

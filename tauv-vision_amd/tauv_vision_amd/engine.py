@@ -45,7 +45,7 @@ class NativeEngine:
     def slices(self, batch):
         """Frame counts of the concurrent slices a forward of `batch` frames launches."""
         n = ctypes.c_int32()
-        sb = (ctypes.c_int32 * 2)()
+        sb = (ctypes.c_int32 * 8)()  # TV_MAX_SLICES
         _lib.check(_lib.lib().tv_engine_slices(self._h, batch, ctypes.byref(n), sb), "slices")
         return [sb[i] for i in range(n.value)]
 

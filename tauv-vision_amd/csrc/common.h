@@ -102,8 +102,10 @@ constexpr int kConv3MaxN = 1024;
 // epi = 0: store the activations; epi = 1: fused 1x1 heads into the fp32 output `out` (head_*)
 // res = 1: two segments — seg 0 the 3x3 input, seg 1 a 1x1 conv (stride seg[1].stride) over a
 // 128-channel tensor summed into the same accumulators (ResidualBlock conv2 + conv_residual)
+// ni = 4: 128-channel tiles; ni = 2: 64-channel half tiles (epi 0 only; p.ntiles still counts
+// 128-channel tiles, the grid covers mtiles * ntiles * 2 work units)
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s, int epi = 0, int res = 0);
+                   hipStream_t s, int epi = 0, int res = 0, int ni = 4);
 int conv3x3_tiles(int B, int H, int W, int tw);
 // Persistent halo-tile 3x3 / stride 2 / pad 1 kernel (conv3x3s2.hip), fp16/bf16, 128 -> 128
 // channels: 16x32-pixel output tiles; ConvParams.mtiles = conv3x3s2_tiles(B, Ho, Wo), ntiles = 1
@@ -113,7 +115,7 @@ int conv3x3s2_repack(const void* w, int Kpad, int esz, void* out, hipStream_t s)
 int launch_conv3x3s2(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int grid, hipStream_t s);
 // k-step-major, pre-swizzled weight copy the kernel streams (from the [Npad][Kpad] packing)
 size_t conv3x3_weight_bytes(int ntiles, int res);
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, void* out, hipStream_t s);
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, void* out, hipStream_t s);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,

@@ -71,6 +71,8 @@ typedef const __attribute__((address_space(1))) void gvoid;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 __device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+__device__ u32x2 raw_buffer_load_v2(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
 __device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
 __device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
                                     int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
@@ -105,9 +107,10 @@ __device__ __forceinline__ void wait_vm_n(int n) {
 template <int V>
 using IC = std::integral_constant<int, V>;
 
+template <int NI>
 struct Half {  // fragments of one 16-deep sub-step
   u32x4 x[2];    // pixel fragments f
-  u32x4 w[4];    // channel fragments i
+  u32x4 w[NI];   // channel fragments i
 };
 
 // 16-byte store of 8 channels from two MFMA register groups (k, k+1) of one 32x32 tile:
@@ -128,10 +131,17 @@ __device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh
   gstore16(dst + 8 * lh, make_uint4(r0[0], r1[0], r0[1], r1[1]));
 }
 
-template <typename T, typename OutT, int TW, int ACT, int EPI, int RES>
+// NI: 32-channel fragments per wave — 4 (a 128-channel tile) or 2 (a 64-channel half tile, twice
+// the work units for layers whose 128-channel tiles leave the last round of CUs mostly idle)
+template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
+  static_assert(NI == 4 || (NI == 2 && EPI == 0), "half tiles: plain epilogue only");
   constexpr int SPTK = spt<RES>();  // k-steps per tile
+  constexpr int BNK = 32 * NI;      // output channels per tile
+  constexpr int WSL = BNK * 64;     // weight bytes per k-step (an LDS ring slot holds up to WSLOT)
+  constexpr int WPL = WSL / 512;    // weight bytes per lane per k-step (16 or 8)
+  using WReg = typename std::conditional<NI == 4, u32x4, u32x2>::type;
   constexpr int TH = P / TW;
   constexpr int RS = TW + 2;                               // halo row stride (pixels)
   constexpr int FOFF = (TW == 32 ? 1 : 2) * RS * PITCH;    // next 32-pixel fragment
@@ -149,7 +159,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int H = sg.H, W = sg.W, ldc = sg.ldc;
   const int tiles_x = (W + TW - 1) / TW;
   const int tiles_f = ((H + TH - 1) / TH) * tiles_x;
-  const int ntiles = p.ntiles;
+  const int ntiles = p.ntiles * (4 / NI);  // channel tiles of BNK (p.ntiles counts 128-channel tiles)
   const int ntot = p.mtiles * ntiles;
   [[maybe_unused]] const unsigned long long out_frame_bytes = (unsigned long long)H * W * p.out_ldc * sizeof(OutT);  // < 2^31 (host)
 
@@ -187,18 +197,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     rsrc.z = (int)(unsigned)((unsigned long long)p.M * ldc * sizeof(T));  // bytes (host checks < 2^31)
     rsrc.w = 0x00020000;
   }
-  // k-step-major weights: [ntile][k-step][128 rows][64 B], chunks pre-swizzled; one 1 KiB
-  // piece per wave per k-step at ((ntile * SPT + q) * 8 + wave) KiB
+  // k-step-major weights: [ntile][k-step][BNK rows][64 B], chunks pre-swizzled; one WSL/8 piece
+  // per wave per k-step at (ntile * SPT + q) * WSL + wave * WSL / 8
   // (read through a buffer resource: one lane-offset VGPR, the k-step offset in an SGPR)
   i32x4 wrsrc;
   {
     const unsigned long long a = (unsigned long long)p.weight;
     wrsrc.x = (int)(unsigned)a;
     wrsrc.y = (int)(unsigned)(a >> 32);
-    wrsrc.z = ntiles * SPTK * WSLOT;
+    wrsrc.z = ntiles * SPTK * WSL;
     wrsrc.w = 0x00020000;
   }
-  const int wvoff = wave * 1024 + lane * 16;
+  const int wvoff = wave * (WSL / 8) + lane * WPL;
 
   // ---- tile decode
   auto tile_of = [&](int idx, int& fr, int& y0, int& x0, int& nt) __attribute__((always_inline)) {
@@ -285,9 +295,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   // register-staged weights: one 16-byte global load per lane per k-step, written to the
   // ring slot with ds_write_b128 one step later (instead of an LDS-DMA piece per k-step)
-  u32x4 wreg[4];  // k-step q's weights are loaded at step q-5 into set q % 4
-  auto w_load = [&](u32x4& dst) __attribute__((always_inline)) {
-    dst = raw_buffer_load_v4(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSLOT, 0);
+  WReg wreg[4];  // k-step q's weights are loaded at step q-5 into set q % 4
+  auto w_load = [&](WReg& dst) __attribute__((always_inline)) {
+    if constexpr (NI == 4) dst = raw_buffer_load_v4(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
+    else dst = raw_buffer_load_v2(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
     if (++wc_in == SPTK) {
       wc_in = 0;
       if (++wc_idx < ntl) {
@@ -320,7 +331,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 
   // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]; TAP 9 = residual k-step
-  auto read_one = [&](auto r, auto j, auto tap, unsigned xb, unsigned wb, Half& F) __attribute__((always_inline)) {
+  auto read_one = [&](auto r, auto j, auto tap, unsigned xb, unsigned wb, Half<NI>& F) __attribute__((always_inline)) {
     constexpr int R = decltype(r)::value, J = decltype(j)::value, TAP = decltype(tap)::value;
     if constexpr (TAP == 9) {
       if constexpr (R < 2) F.x[R] = ds_read16<R * 2048>(rxa[J]);
@@ -332,11 +343,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     }
   };
 
-  f32x16 acc[2][4];  // [pixel fragment f][channel fragment i]; first written by a tile's first k-step
+  f32x16 acc[2][NI];  // [pixel fragment f][channel fragment i]; first written by a tile's first k-step
 
   // the 2 MFMAs of channel fragment I of one sub-step; FIRST: the tile's first products
   // (accumulate onto zero instead of clearing the accumulators in the epilogue)
-  auto mfma_pair = [&](auto i, auto first, const Half& F) __attribute__((always_inline)) {
+  auto mfma_pair = [&](auto i, auto first, const Half<NI>& F) __attribute__((always_inline)) {
     constexpr int I = decltype(i)::value;
     if constexpr (decltype(first)::value) {
       acc[0][I] = f32x16{};
@@ -348,7 +359,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 
   // ---- epilogue of the tile (fr, y0, x0, nt): straight from the accumulators
   auto epilogue = [&](int fr, int y0, int x0, int nt) __attribute__((always_inline)) {
-    const int n0 = nt * BN;
+    const int n0 = nt * BNK;
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       const int q = WP * wave + 32 * f + l32;
@@ -371,7 +382,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       }
       [[maybe_unused]] f32x16 hacc = f32x16{};  // EPI 1: the 1x1 heads' partial sums of this pixel
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
           float v[2][4];
@@ -446,8 +457,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // which drains the halo pieces and weight loads issued since (measured: ~20% of the layer).
   w_load(wreg[0]);
   w_load(wreg[1]);
-  *reinterpret_cast<u32x4*>(smem + OFF_W + wave * 1024 + lane * 16) = wreg[0];
-  *reinterpret_cast<u32x4*>(smem + OFF_W + WSLOT + wave * 1024 + lane * 16) = wreg[1];
+  *reinterpret_cast<WReg*>(smem + OFF_W + wvoff) = wreg[0];
+  *reinterpret_cast<WReg*>(smem + OFF_W + WSLOT + wvoff) = wreg[1];
   w_load(wreg[2]);
   w_load(wreg[3]);
   w_load(wreg[0]);
@@ -462,22 +473,24 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     nul.z = 0;
     nul.w = 0x00020000;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) raw_buffer_store_v4(u32x4{0u, 0u, 0u, 0u}, nul, k * 16, 0, 0);
+    for (int k = 0; k < 4 * NI; ++k) raw_buffer_store_v4(u32x4{0u, 0u, 0u, 0u}, nul, k * 16, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
   // the halo (issued first) landed; the weights of k-steps 2..4 (and the dropped stores) may stay in flight
-  wait_vm<EPI == 0 ? 19 : 3>();
+  wait_vm<EPI == 0 ? 3 + 4 * NI : 3>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 
-  Half H0, H1;  // sub-step 0 / 1 fragments
+  Half<NI> H0, H1;  // sub-step 0 / 1 fragments
   read_one(IC<0>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   read_one(IC<1>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   read_one(IC<2>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   read_one(IC<3>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+  if constexpr (NI == 4) {
+    read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+    read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+  }
   if (p.stamps) st1 = __builtin_amdgcn_s_memtime();
 
   int s = 0;   // global k-step
@@ -533,7 +546,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     read_one(IC<3>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     // k-step s+2 (loaded at step s-3) into its ring slot: it last held k-step s-1, read
     // completely before this step's barrier (past the end: an unread slot)
-    *reinterpret_cast<u32x4*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = wreg[(PAR + 2) & 3];
+    *reinterpret_cast<WReg*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wvoff) = wreg[(PAR + 2) & 3];
     if constexpr (TAP == 0) {
       if (nxt_exists && nxt_newtile) {
         int fr, y0, x0, nt;
@@ -541,15 +554,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         halo_offsets(fr, y0, x0);
       }
     }
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<2>{}, IC<FIRST>{}, H0);
-    read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+    if constexpr (NI == 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_pair(IC<2>{}, IC<FIRST>{}, H0);
+      read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+      read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
+    }
     if constexpr (TAP < HTAPS)
       halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);  // (no next block: the idle buffer)
     if constexpr (RES && TAP >= 1 && TAP <= RPW) res_piece(TAP - 1, cur_fr, cur_y0, cur_x0, cb);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<3>{}, IC<FIRST>{}, H0);
+    if constexpr (NI == 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_pair(IC<3>{}, IC<FIRST>{}, H0);
+    }
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
     __builtin_amdgcn_sched_barrier(0);
@@ -567,14 +584,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       read_one(IC<2>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
       read_one(IC<3>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<2>{}, IC<false>{}, H1);
-    if (do_r) {
-      read_one(IC<4>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-      read_one(IC<5>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
+    if constexpr (NI == 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_pair(IC<2>{}, IC<false>{}, H1);
+      if (do_r) {
+        read_one(IC<4>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
+        read_one(IC<5>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_pair(IC<3>{}, IC<false>{}, H1);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<3>{}, IC<false>{}, H1);
     __builtin_amdgcn_sched_barrier(0);
     ++s;
   };
@@ -622,24 +641,25 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 }
 
-// [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q][128 rows][4 x 16 B], q = cb*9 + tap
-// (res: q = cb*10 + j, j = 9 the residual segment's channel block cb at K offset 9*128), slot s
-// of row r holding chunk s ^ ((r >> 2) & 3) of the k-step
-__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, int res, uint4* __restrict__ out) {
+// [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q][bnk rows][4 x 16 B] (channel tiles
+// of bnk = 128 or 64 rows), q = cb*9 + tap (res: q = cb*10 + j, j = 9 the residual segment's
+// channel block cb at K offset 9*128), slot s of row r holding chunk s ^ ((r >> 2) & 3) of the k-step
+__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, int res, int bnk,
+                               uint4* __restrict__ out) {
   const int sp = res ? spt<1>() : spt<0>();
-  const int n = ntiles * sp * BN * 4;
+  const int n = ntiles * sp * BN * 4;  // ntiles of 128 rows
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
-    const int slot = o & 3, row = (o >> 2) & (BN - 1), q = (o >> 9) % sp, nt = (o >> 9) / sp;
+    const int slot = o & 3, row = (o >> 2) % bnk, q = (o / (4 * bnk)) % sp, nt = (o / (4 * bnk)) / sp;
     const int chunk = slot ^ ((row >> 2) & 3);
     const int cb = q / (9 + res), tap = q - cb * (9 + res);
     const int k16 = (tap * 128 + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements); tap 9 = residual
-    out[o] = w[(size_t)(nt * BN + row) * kpad16 + k16];
+    out[o] = w[(size_t)(nt * bnk + row) * kpad16 + k16];
   }
 }
 
-template <typename T, int TW, int ACT, int EPI = 0, int RES = 0>
+template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4>
 static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
-  auto k = conv3x3<T, T, TW, ACT, EPI, RES>;
+  auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI>;
   constexpr int lds = lds_bytes<RES>();
   static bool attr = false;
   if (!attr) {
@@ -666,22 +686,22 @@ size_t conv3x3_weight_bytes(int ntiles, int res) {
   return (size_t)ntiles * (res ? c3::spt<1>() : c3::spt<0>()) * c3::WSLOT;
 }
 
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, void* out, hipStream_t s) {
-  if ((Kpad * esz) % 16 || Kpad < (res ? 10 : 9) * 128) {
-    set_error("conv3x3_repack: bad Kpad");
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, void* out, hipStream_t s) {
+  if ((Kpad * esz) % 16 || Kpad < (res ? 10 : 9) * 128 || (ni != 4 && ni != 2)) {
+    set_error("conv3x3_repack: bad Kpad / ni");
     return 1;
   }
   hipLaunchKernelGGL(c3::repack_weights, dim3(256), dim3(256), 0, s, (const uint4*)w, Kpad * esz / 16, ntiles, res,
-                     (uint4*)out);
+                     32 * ni, (uint4*)out);
   TV_HIP(hipGetLastError());
   return 0;
 }
 
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s, int epi, int res) {
+                   hipStream_t s, int epi, int res, int ni) {
   using namespace c3;
-  if (p.act < 0 || p.act > 2) {
-    set_error("conv3x3: bad activation");
+  if (p.act < 0 || p.act > 2 || (ni != 4 && ni != 2) || (ni == 2 && epi != 0)) {
+    set_error("conv3x3: bad activation / channel tile");
     return 1;
   }
   if (res) {  // ResidualBlock conv2 + conv_residual: ReLU, plain stores
@@ -689,8 +709,13 @@ int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dty
       set_error("conv3x3: residual k-steps need ReLU, one channel tile and two segments");
       return 1;
     }
-    if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 1, 0, 1>(p, dp, out, grid, s) : launch_t<_Float16, 16, 1, 0, 1>(p, dp, out, grid, s);
-    if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 1, 0, 1>(p, dp, out, grid, s) : launch_t<__bf16, 16, 1, 0, 1>(p, dp, out, grid, s);
+    using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
+    static const L r16[2][2] = {{launch_t<_Float16, 16, 1, 0, 1, 2>, launch_t<_Float16, 16, 1, 0, 1, 4>},
+                                {launch_t<_Float16, 32, 1, 0, 1, 2>, launch_t<_Float16, 32, 1, 0, 1, 4>}};
+    static const L rb16[2][2] = {{launch_t<__bf16, 16, 1, 0, 1, 2>, launch_t<__bf16, 16, 1, 0, 1, 4>},
+                                 {launch_t<__bf16, 32, 1, 0, 1, 2>, launch_t<__bf16, 32, 1, 0, 1, 4>}};
+    if (dtype == F16) return r16[tw == 32][ni == 4](p, dp, out, grid, s);
+    if (dtype == BF16) return rb16[tw == 32][ni == 4](p, dp, out, grid, s);
     set_error("conv3x3: fp16/bf16 only");
     return 1;
   }
@@ -705,12 +730,18 @@ int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dty
     return 1;
   }
   using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
-  static const L f16[2][3] = {{launch_t<_Float16, 16, 0>, launch_t<_Float16, 16, 1>, launch_t<_Float16, 16, 2>},
-                              {launch_t<_Float16, 32, 0>, launch_t<_Float16, 32, 1>, launch_t<_Float16, 32, 2>}};
-  static const L b16[2][3] = {{launch_t<__bf16, 16, 0>, launch_t<__bf16, 16, 1>, launch_t<__bf16, 16, 2>},
-                              {launch_t<__bf16, 32, 0>, launch_t<__bf16, 32, 1>, launch_t<__bf16, 32, 2>}};
-  if (dtype == F16) return f16[tw == 32][p.act](p, dp, out, grid, s);
-  if (dtype == BF16) return b16[tw == 32][p.act](p, dp, out, grid, s);
+  static const L f16[2][2][3] = {
+      {{launch_t<_Float16, 16, 0, 0, 0, 2>, launch_t<_Float16, 16, 1, 0, 0, 2>, launch_t<_Float16, 16, 2, 0, 0, 2>},
+       {launch_t<_Float16, 32, 0, 0, 0, 2>, launch_t<_Float16, 32, 1, 0, 0, 2>, launch_t<_Float16, 32, 2, 0, 0, 2>}},
+      {{launch_t<_Float16, 16, 0>, launch_t<_Float16, 16, 1>, launch_t<_Float16, 16, 2>},
+       {launch_t<_Float16, 32, 0>, launch_t<_Float16, 32, 1>, launch_t<_Float16, 32, 2>}}};
+  static const L b16[2][2][3] = {
+      {{launch_t<__bf16, 16, 0, 0, 0, 2>, launch_t<__bf16, 16, 1, 0, 0, 2>, launch_t<__bf16, 16, 2, 0, 0, 2>},
+       {launch_t<__bf16, 32, 0, 0, 0, 2>, launch_t<__bf16, 32, 1, 0, 0, 2>, launch_t<__bf16, 32, 2, 0, 0, 2>}},
+      {{launch_t<__bf16, 16, 0>, launch_t<__bf16, 16, 1>, launch_t<__bf16, 16, 2>},
+       {launch_t<__bf16, 32, 0>, launch_t<__bf16, 32, 1>, launch_t<__bf16, 32, 2>}}};
+  if (dtype == F16) return f16[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
+  if (dtype == BF16) return b16[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
   set_error("conv3x3: fp16/bf16 only");
   return 1;
 }

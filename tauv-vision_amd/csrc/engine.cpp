@@ -249,6 +249,8 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_C3_NI")) c3_ni_force = std::atoi(env) == 2 ? 2 : std::atoi(env) == 4 ? 4 : 0;
+  if (const char* env = std::getenv("TV_C3_HALF_COST")) c3_half_cost = std::atoi(env);
   if (const char* env = std::getenv("TV_SLICES")) slices = std::max(1, std::min(kMaxSlices, std::atoi(env)));
   if (const char* env = std::getenv("TV_SLICE_SIZES")) {
     for (const char* c = env; *c;) {
@@ -280,6 +282,7 @@ Engine::~Engine() {
   for (auto& p : packed) {
     if (p.w) (void)hipFree(p.w);
     if (p.w_c3) (void)hipFree(p.w_c3);
+    if (p.w_c3h) (void)hipFree(p.w_c3h);
     if (p.head_w) (void)hipFree(p.head_w);
     if (p.head_b) (void)hipFree(p.head_b);
     if (p.bias) (void)hipFree(p.bias);
@@ -402,6 +405,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->c3_grid.assign(plan.ops.size(), 0);
   ws->s2_grid.assign(plan.ops.size(), 0);
   ws->c3_res.assign(plan.ops.size(), 0);
+  ws->c3_ni.assign(plan.ops.size(), 4);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (op.kind == OP_PREP) continue;
@@ -483,18 +487,27 @@ int Engine::make_workspace(int B, Workspace* ws) {
         const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16), t32 = conv3x3_tiles(B, cs.H, cs.W, 32);
         const int tw = c3_tw_force ? c3_tw_force : t32 <= t16 ? 32 : 16;
         const int mt = tw == 32 ? t32 : t16;
-        long total = (long)mt * p.ntiles;
+        // 64-channel half tiles when the last round of 128-channel tiles would leave most CUs
+        // idle: a half tile costs ~c3_half_cost of a full one (two work units per tile)
+        const long t4 = (long)mt * p.ntiles;
+        const long r4 = (t4 + cu_count - 1) / cu_count, r2 = (2 * t4 + cu_count - 1) / cu_count;
+        int ni = c3_ni_force ? c3_ni_force : (c3_half_cost > 0 && c3_half_cost * r2 < 100 * r4) ? 2 : 4;
+        if (op.act == 2 && !res && op.out >= 0 && i + 1 < plan.ops.size() && !plan.ops[i + 1].diag_in_off.empty())
+          ni = 4;  // the stacked heads (fused 1x1 epilogue) keep 128-channel tiles
+        const long total = t4 * (4 / ni);
         int grid = (int)std::min<long>(total, cu_count);
         if (grid >= 8) grid -= grid % 8;
         Packed& pk3 = packed[i];
-        if (!pk3.w_c3) {
-          TV_HIP(hipMalloc(&pk3.w_c3, conv3x3_weight_bytes(p.ntiles, res)));
-          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, pk3.w_c3, nullptr);
+        void*& wc = ni == 4 ? pk3.w_c3 : pk3.w_c3h;
+        if (!wc) {
+          TV_HIP(hipMalloc(&wc, conv3x3_weight_bytes(p.ntiles, res)));
+          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, ni, wc, nullptr);
           if (rc) return rc;
           TV_HIP(hipDeviceSynchronize());
         }
-        p.weight = pk3.w_c3;
+        p.weight = wc;
         ws->c3_tw[i] = tw;
+        ws->c3_ni[i] = ni;
         ws->c3_res[i] = res;
         ws->c3_grid[i] = grid;
         ws->halo_tw[i] = 0;
@@ -536,7 +549,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   for (size_t i = 0; headfuse_mode && i + 1 < plan.ops.size(); ++i) {
     const OpSpec& h2 = plan.ops[i + 1];
     const Packed& pk2 = packed[i + 1];
-    if (!ws->c3_tw[i] || h2.diag_in_off.empty() || !pk2.head_ok || h2.out >= 0 || h2.segs[0].src != plan.ops[i].out ||
+    if (!ws->c3_tw[i] || ws->c3_ni[i] != 4 || h2.diag_in_off.empty() || !pk2.head_ok || h2.out >= 0 || h2.segs[0].src != plan.ops[i].out ||
         plan.ops[i].act != 2 || ws->params[i].ntiles != plan.ops[i].N / 128)
       continue;
     ConvParams& p = ws->params[i];
@@ -672,7 +685,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
-                                           ws->c3_res[i])
+                                           ws->c3_res[i], ws->c3_ni[i])
            : ws->halo_tw[i] ? launch_conv_halo(p, ws->dparams + i, p.out, dtype, out_f32, ws->halo_tw[i], s)
            : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
                              : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
@@ -803,7 +816,7 @@ const char* Engine::op_kernel(int B, size_t i) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
-      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ">";
+      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ">";
       else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";

@@ -14,6 +14,7 @@ namespace tv {
 struct Packed {
   void* w = nullptr;       // [Npad][Kpad] compute dtype
   void* w_c3 = nullptr;    // conv3x3.hip / conv3x3s2.hip k-step-major copy (made on first use)
+  void* w_c3h = nullptr;   // conv3x3.hip copy for 64-channel half tiles (ni = 2)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;
@@ -36,6 +37,7 @@ struct Workspace {
   std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
   std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
   std::vector<int> c3_res;          // per op: 1 = conv3x3 with the 1x1 residual segment (RES)
+  std::vector<int> c3_ni;           // per op: channel fragments per wave (4: 128-channel tiles, 2: 64)
   std::vector<int> s2_grid;         // per op: > 0 = persistent stride-2 conv3x3s2 (workgroups)
   std::vector<int> head_fused;      // per op: 1 = stacked 3x3 heads with the 1x1 heads fused in
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
@@ -56,6 +58,8 @@ struct Engine {
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
   int pipe_mode = 1;           // -1 auto (>= 256 tiles), 0 never, 1 whenever representable (env TV_CONV_PIPE)
   int c3_tw_force = 0;         // conv3x3 tile width override (env TV_C3_TW = 16 / 32)
+  int c3_ni_force = 0;         // conv3x3 channel tile: 0 = by grid rounds, 2 / 4 forced (env TV_C3_NI)
+  int c3_half_cost = 55;       // cost of a 64-channel half tile in % of a full one (env TV_C3_HALF_COST, 0 = never)
   int conv3_min_pix = 100;     // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)
   int s2_mode = 1;             // stride-2 halo kernel for eligible fp16/bf16 layers (env TV_CONV3S2=0 off)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)

@@ -249,6 +249,8 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_S2_MINTILES")) s2_min_tiles = std::atoi(env);
+  if (const char* env = std::getenv("TV_SKIP_KINDS")) skip_kinds = std::atoi(env);
   if (const char* env = std::getenv("TV_C3_NI")) c3_ni_force = std::atoi(env) == 2 ? 2 : std::atoi(env) == 4 ? 4 : 0;
   if (const char* env = std::getenv("TV_C3_HALF_COST")) c3_half_cost = std::atoi(env);
   if (const char* env = std::getenv("TV_SLICES")) slices = std::max(1, std::min(kMaxSlices, std::atoi(env)));
@@ -525,7 +527,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const int mt = conv3x3s2_tiles(B, p.Ho, p.Wo);
       if (sg.kh == 3 && sg.kw == 3 && sg.stride == 2 && sg.pad == 1 && pw == 1 && !sg.row_expand && cs.C == 128 &&
           p.N == 128 && p.ntiles == 1 && cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && frame_bytes < (1ull << 31) &&
-          mt >= cu_count) {
+          mt >= (s2_min_tiles >= 0 ? s2_min_tiles : cu_count)) {
         Packed& pk3 = packed[i];
         if (!pk3.w_c3) {
           TV_HIP(hipMalloc(&pk3.w_c3, conv3x3s2_weight_bytes()));
@@ -644,6 +646,11 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const OpSpec& op = plan.ops[i];
   char* base = (char*)ws->arena;
   if (stem_op >= 0 && op.kind == OP_PREP) return TV_OK;  // staging runs inside the stem kernel
+  if (skip_kinds) {  // what-if timing diagnostic (env TV_SKIP_KINDS): results are garbage
+    const int kind = (int)i == stem_op ? 8 : ws->head_fused[i] ? 32 : ws->convt[i] ? 2 : ws->s2_grid[i] ? 4
+                     : ws->c3_tw[i] ? 16 : (op.kind == OP_CONV || op.kind == OP_CONVT_ADD) && !ws->head_skip[i] ? 1 : 0;
+    if (skip_kinds & kind) return TV_OK;
+  }
   if ((int)i == stem_op) {
     StemParams sp{};
     sp.input = input;

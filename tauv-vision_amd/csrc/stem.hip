@@ -206,37 +206,35 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const char* abrow = ab0 + lh * (TW * EPIX - 32);
   const char* wfl = smem + OFF_W + lane * 16;
 
+  // one output row f of the wave's two: its 16 KiB of stores (epilogue) then drain under the
+  // other row's MFMAs instead of all 128 KiB of a tile leaving at once
   f32x16 acc[2][4];
-  auto mfma_tile = [&](int ebuf) __attribute__((always_inline)) {
+  auto mfma_row = [&](int ebuf, auto fc) __attribute__((always_inline)) {
+    constexpr int f = decltype(fc)::value;
 #pragma unroll
-    for (int f = 0; f < 2; ++f)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[f][i] = f32x16{};
+    for (int i = 0; i < 4; ++i) acc[f][i] = f32x16{};
 #pragma unroll
     for (int j = 0; j < KS; ++j) {
       const int c0 = 2 * j;  // lane half 0's chunk
       const int off0 = (c0 / 3) * TW * EPIX + (c0 % 3) * 16 + ebuf * EBUF;
       const char* base = j == KS - 1 ? ab0 : (c0 % 3 == 2 ? abrow : ab16);
-      uint4 a[2], b[4];
-#pragma unroll
-      for (int f = 0; f < 2; ++f) a[f] = *reinterpret_cast<const uint4*>(base + off0 + f * TW * EPIX);
+      uint4 b[4];
+      const uint4 a = *reinterpret_cast<const uint4*>(base + off0 + f * TW * EPIX);
 #pragma unroll
       for (int i = 0; i < 4; ++i) b[i] = *reinterpret_cast<const uint4*>(wfl + (j * 4 + i) * 1024);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int f = 0; f < 2; ++f) Mfma<T>::run(b[i], a[f], acc[f][i]);
+      for (int i = 0; i < 4; ++i) Mfma<T>::run(b[i], a, acc[f][i]);
     }
   };
 
-  auto epilogue = [&](int t) __attribute__((always_inline)) {
+  auto epilogue = [&](int t, auto fc) __attribute__((always_inline)) {
+    constexpr int f = decltype(fc)::value;
     const int fr = t / tiles_f;
     const int r = t - fr * tiles_f;
     const int ty = r / tiles_x;
     const int y0 = ty * TH, x0 = (r - ty * tiles_x) * TW;
     const float* lb = reinterpret_cast<const float*>(smem + OFF_B);
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
+    {
       const int y = y0 + 2 * wave + f, x = x0 + l32;
       const bool ok = y < H && x < W;
       T* dst = reinterpret_cast<T*>(p.out) + ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.out_ldc;
@@ -276,8 +274,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto tile = [&](int t, int eb, unsigned (&raw_next)[NS], unsigned (&raw_k2)[NS]) __attribute__((always_inline)) {
     const int tn = t + G, tn2 = t + 2 * G;
     if (tn2 < ntot && !(p.ablate & 4)) load_window(tn2, raw_k2);  // tile k's set: already consumed
-    if (!(p.ablate & 2)) mfma_tile(eb);
-    epilogue(t);
+    if (!(p.ablate & 2)) mfma_row(eb, std::integral_constant<int, 0>{});
+    epilogue(t, std::integral_constant<int, 0>{});
+    if (!(p.ablate & 2)) mfma_row(eb, std::integral_constant<int, 1>{});
+    epilogue(t, std::integral_constant<int, 1>{});
     if (tn < ntot && !(p.ablate & 4)) {
       store_window(tn, raw_next);  // N is free: its last reader (expand) finished before the last barrier
       lds_barrier();

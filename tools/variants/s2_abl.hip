@@ -24,6 +24,11 @@
 
 #include <type_traits>
 
+// Ablation variant (timing only, wrong results): S2_ABL bits 1 main-loop halo DMA, 2 weight staging,
+// 4 halo reads from tile 0 of frame 0 only (L2-resident source)
+#ifndef S2_ABL
+#define S2_ABL 0
+#endif
 namespace tv {
 namespace c3s2 {
 
@@ -54,37 +59,6 @@ constexpr int J_TY[9] = {0, 0, 1, 1, 0, 1, 0, 0, 0};
 constexpr int J_TX[9] = {0, 1, 0, 1, 0, 0, 0, 1, 0};
 // original tap ky*3+kx of k-step j: ky = 2ty + 1 - p, kx = 2tx + 1 - q
 constexpr int J_TAP[9] = {0, 2, 6, 8, 1, 7, 3, 5, 4};
-
-// Block order of a tile: channel blocks in pairs (c0, c1) = (2P, 2P+1), and within a pair the
-// two channel blocks' copies of one phase block back to back — a pixel's 32-channel halves of
-// one 128-byte line are then fetched a block apart (the second from L2) instead of a whole
-// channel block (9 k-steps) apart, when the first half has left the L2. The 1-k-step (0,0)
-// blocks sit between the longer ones so every block n+2, issued at the start of block n, has
-// >= 3 k-steps to land.
-constexpr int NBLK = 8;                               // blocks per channel-block pair
-constexpr int BLK_PB[NBLK] = {0, 0, 3, 1, 1, 3, 2, 2};  // phase block: 0 (1,1), 1 (1,0), 2 (0,1), 3 (0,0)
-constexpr int BLK_CB[NBLK] = {0, 1, 0, 0, 1, 1, 0, 1};  // channel block within the pair
-constexpr int PB_LEN[4] = {4, 2, 2, 1};
-constexpr int PB_J0[4] = {0, 4, 6, 8};                // first k-step j of the phase block
-struct Sched {
-  int cb[SPT], j[SPT], blk[SPT], t[SPT];
-};
-constexpr Sched make_sched() {
-  Sched sc{};
-  int q = 0;
-  for (int P = 0; P < NCB / 2; ++P)
-    for (int b = 0; b < NBLK; ++b)
-      for (int t = 0; t < PB_LEN[BLK_PB[b]]; ++t) {
-        sc.cb[q] = 2 * P + BLK_CB[b];
-        sc.j[q] = PB_J0[BLK_PB[b]] + t;
-        sc.blk[q] = P * NBLK + b;
-        sc.t[q] = t;
-        ++q;
-      }
-  return sc;
-}
-constexpr Sched SCH = make_sched();
-static_assert(SCH.blk[SPT - 1] == 2 * NBLK - 1 && SCH.j[SPT - 1] == PB_J0[BLK_PB[NBLK - 1]] + 1, "schedule covers the tile");
 
 typedef __attribute__((address_space(3))) char lds_char;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -119,22 +93,12 @@ __device__ __forceinline__ void wait_vm_n(int n) {
     case 8: wait_vm<8>(); break;
     case 9: wait_vm<9>(); break;
     case 10: wait_vm<10>(); break;
-    case 11: wait_vm<11>(); break;
-    case 12: wait_vm<12>(); break;
-    default: wait_vm<13>(); break;
+    default: wait_vm<11>(); break;
   }
 }
 
 template <int V>
 using IC = std::integral_constant<int, V>;
-
-template <int Q, int N, typename F>
-__device__ __forceinline__ void unroll(F& f) {
-  if constexpr (Q < N) {
-    f(IC<Q>{});
-    unroll<Q + 1, N>(f);
-  }
-}
 
 struct Half {  // fragments of one 16-deep sub-step
   u32x4 x[2];  // pixel fragments f
@@ -220,6 +184,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   // issue the halo of phase block pb, channel block cb of tile (fr, y0, x0) into buffer buf
   auto issue_block = [&](int fr, int y0, int x0, int cb, int pb, int buf, auto loc, auto hic) __attribute__((always_inline)) {
+    if constexpr (S2_ABL & 4) { fr = 0; y0 = 0; x0 = 0; }
     constexpr int LO = decltype(loc)::value, HI = decltype(hic)::value;
     const int pr = pb < 2 ? 1 : 0, pc = (pb & 1) == 0 ? 1 : 0;  // PB_P, PB_Q
     const i32x4 rs = rsrc_of(fr);
@@ -325,8 +290,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // ---- prologue: halos of blocks 0, 1 of tile 0 (buffers 0, 1), weights of k-steps 0..2
   int cur_fr, cur_y0, cur_x0;
   tile_of(0, cur_fr, cur_y0, cur_x0);
-  issue_block(cur_fr, cur_y0, cur_x0, SCH.cb[0], BLK_PB[0], 0, IC<0>{}, IC<HPW>{});
-  issue_block(cur_fr, cur_y0, cur_x0, BLK_CB[1], BLK_PB[1], 1, IC<0>{}, IC<HPW>{});
+  issue_block(cur_fr, cur_y0, cur_x0, 0, 0, 0, IC<0>{}, IC<HPW>{});
+  issue_block(cur_fr, cur_y0, cur_x0, 0, 1, 1, IC<0>{}, IC<HPW>{});
   __builtin_amdgcn_sched_barrier(0);  // the counted wait below needs the halos issued first
   w_load(wreg[0]);
   w_load(wreg[1]);
@@ -354,45 +319,46 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   int nx_fr = 0, nx_y0 = 0, nx_x0 = 0;  // the next tile (target of the next channel block's halos at cb 3)
   bool nx_exists = false;
 
-  // One k-step: compile-time position Q in the tile's schedule (SCH): channel block CB, k-step
-  // J of it, block BLK (0..15) and step TB within the block.
-  auto step = [&](auto qc) __attribute__((always_inline)) {
-    constexpr int Q = decltype(qc)::value;
-    constexpr int CB = SCH.cb[Q], J = SCH.j[Q], BLK = SCH.blk[Q], TB = SCH.t[Q];
-    constexpr int B8 = BLK % NBLK;
-    constexpr int L = PB_LEN[BLK_PB[B8]], LPREV = PB_LEN[BLK_PB[(B8 + NBLK - 1) % NBLK]];
-    constexpr bool BOUNDARY = TB == L - 1;  // the next k-step starts a new block
-    // VMEM operations issued after the last piece of the next block's halo (exact): it was
-    // issued at the start of the previous block, before that step's weight load; since then one
-    // weight load per k-step and, if this block is longer than one k-step, this block's own issue
-    // (at its first step, before that step's weight load)
-    constexpr int YOUNGER = LPREV + L - 1 + (L >= 2 ? HPW : 0);
-    static_assert(YOUNGER <= 13, "wait_vm_n range");
-    if constexpr (BOUNDARY) wait_vm_n(s + 1 < S_tot ? YOUNGER : 0);
+  // One k-step: compile-time channel block CB and k-step J of it.
+  auto step = [&](auto cbc, auto jc, auto first, auto par) __attribute__((always_inline)) {
+    constexpr int CB = decltype(cbc)::value, J = decltype(jc)::value;
+    constexpr bool BOUNDARY = J == 3 || J == 5 || J == 7 || J == 8;  // the next k-step starts a new block
+    auto wl = [&](int q) { return q >= 0 ? 1 : 0; };  // a weight load is issued at every step q >= 0
+    // VMEM operations issued after the last piece of the halo the next k-step reads (exact);
+    // within a step the halo pieces (J 0, 4, 6, 8) precede the weight load
+    int younger = 0;
+    if constexpr (J == 3) younger = wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + HPW;
+    if constexpr (J == 5) younger = wl(s - 5) + wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + HPW;
+    if constexpr (J == 7) younger = wl(s - 3) + wl(s - 2) + wl(s - 1) + HPW;
+    if constexpr (J == 8) younger = wl(s - 2) + wl(s - 1);
+    if constexpr (BOUNDARY) wait_vm_n(s + 1 < S_tot ? younger : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 
-    constexpr int NJ = SCH.j[(Q + 1) % SPT];  // next k-step's j
+    constexpr int NJ = J == 8 ? 0 : J + 1;  // next k-step's j
     const bool do_r = s + 1 < S_tot;
     const int nbuf = BOUNDARY ? (buf == NBUF - 1 ? 0 : buf + 1) : buf;
     const unsigned xc = xa + (unsigned)(buf * HBUF);
     const unsigned xn = xa + (unsigned)(nbuf * HBUF);
     const unsigned wc1 = wa[1] + (unsigned)((s % RING) * WSLOT);
     const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
-    constexpr bool FIRST = Q == 0;
-    constexpr int PAR = Q & 3;  // SPT % 4 == 0: the weight register set is static
-    // at a block's first k-step: block BLK + 2 (this tile or the next one) into the buffer block
-    // BLK - 1 used (free since this step's barrier), two pieces after each of the first half's
-    // MFMA pairs (an LDS-DMA instruction holds its wave at issue)
-    constexpr int NB = BLK + 2, NB8 = NB % NBLK;
-    constexpr bool NEXT_TILE = NB >= 2 * NBLK;
-    constexpr int ICB = 2 * ((NB % (2 * NBLK)) / NBLK) + BLK_CB[NB8], IPB = BLK_PB[NB8];
+    constexpr bool FIRST = CB == 0 && J == 0 && decltype(first)::value;
+    constexpr int PAR = decltype(par)::value;
+    // halo of block n + 2 into the buffer block n - 1 used (free since this step's barrier),
+    // two pieces after each of the first half's MFMA pairs: an LDS-DMA instruction holds its
+    // wave at issue, six in a row idled the matrix core (the whole DMA cost 30% of the layer)
     auto issue_part = [&](auto lo, auto hi) __attribute__((always_inline)) {
-      if constexpr (TB == 0) {
-        const int tbuf = buf == 0 ? 2 : buf - 1;  // (buf + 2) % 3
-        if constexpr (NEXT_TILE) issue_block(nx_fr, nx_y0, nx_x0, ICB, IPB, tbuf, lo, hi);  // (last tile: itself, into a free buffer)
-        else issue_block(cur_fr, cur_y0, cur_x0, ICB, IPB, tbuf, lo, hi);
+      if constexpr (S2_ABL & 1) return;
+      const int tbuf = buf == 0 ? 2 : buf - 1;  // (buf + 2) % 3
+      if constexpr (J == 0) issue_block(cur_fr, cur_y0, cur_x0, CB, 2, tbuf, lo, hi);
+      if constexpr (J == 4) issue_block(cur_fr, cur_y0, cur_x0, CB, 3, tbuf, lo, hi);
+      if constexpr (J == 6 || J == 8) {
+        if constexpr (CB + 1 < NCB) {
+          issue_block(cur_fr, cur_y0, cur_x0, CB + 1, J == 6 ? 0 : 1, tbuf, lo, hi);
+        } else {
+          issue_block(nx_fr, nx_y0, nx_x0, 0, J == 6 ? 0 : 1, tbuf, lo, hi);  // (last tile: itself, into a free buffer)
+        }
       }
     };
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
@@ -440,12 +406,29 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     ++s;
   };
 
+  auto cblock = [&](auto cbc) __attribute__((always_inline)) {
+    constexpr int CB = decltype(cbc)::value;
+    constexpr int P0 = CB * 9;  // k-step index within the tile (SPT % 4 == 0: the set is static)
+    step(cbc, IC<0>{}, IC<1>{}, IC<(P0 + 0) & 3>{});
+    step(cbc, IC<1>{}, IC<0>{}, IC<(P0 + 1) & 3>{});
+    step(cbc, IC<2>{}, IC<0>{}, IC<(P0 + 2) & 3>{});
+    step(cbc, IC<3>{}, IC<0>{}, IC<(P0 + 3) & 3>{});
+    step(cbc, IC<4>{}, IC<0>{}, IC<(P0 + 4) & 3>{});
+    step(cbc, IC<5>{}, IC<0>{}, IC<(P0 + 5) & 3>{});
+    step(cbc, IC<6>{}, IC<0>{}, IC<(P0 + 6) & 3>{});
+    step(cbc, IC<7>{}, IC<0>{}, IC<(P0 + 7) & 3>{});
+    step(cbc, IC<8>{}, IC<0>{}, IC<(P0 + 8) & 3>{});
+  };
+
   static_assert(NCB == 4 && SPT % 4 == 0, "tile body is unrolled for 4 channel blocks; 4 weight register sets");
   for (; tl < ntl;) {
     nx_exists = tl + 1 < ntl;
     if (nx_exists) tile_of(tl + 1, nx_fr, nx_y0, nx_x0);
     else nx_fr = cur_fr, nx_y0 = cur_y0, nx_x0 = cur_x0;
-    unroll<0, SPT>(step);  // the whole tile, straight-line
+    cblock(IC<0>{});
+    cblock(IC<1>{});
+    cblock(IC<2>{});
+    cblock(IC<3>{});
     epilogue(cur_fr, cur_y0, cur_x0);
     ++tl;
     cur_fr = nx_fr;
@@ -454,15 +437,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 }
 
-// [Npad][Kpad] (K = tap * 128 + channel) -> [k-step q][128 rows][4 x 16 B] in this kernel's
-// schedule (channel block SCH.cb[q], tap J_TAP[SCH.j[q]]), slot s of row r holding chunk
-// s ^ ((r >> 2) & 3)
+// [Npad][Kpad] (K = tap * 128 + channel) -> [k-step q = cb*9 + j][128 rows][4 x 16 B] in this
+// kernel's phase-block k-step order (tap J_TAP[j]), slot s of row r holding chunk s ^ ((r >> 2) & 3)
 __global__ void repack_weights_s2(const uint4* __restrict__ w, int kpad16, uint4* __restrict__ out) {
   const int n = SPT * BN * 4;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
     const int slot = o & 3, row = (o >> 2) & (BN - 1), q = o >> 9;
     const int chunk = slot ^ ((row >> 2) & 3);
-    const int cb = SCH.cb[q], j = SCH.j[q];
+    const int cb = q / 9, j = q - cb * 9;
     const int k16 = (J_TAP[j] * 128 + cb * CBK) / 8 + chunk;
     out[o] = w[(size_t)row * kpad16 + k16];
   }

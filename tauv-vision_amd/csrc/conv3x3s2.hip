@@ -354,11 +354,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   int nx_fr = 0, nx_y0 = 0, nx_x0 = 0;  // the next tile (target of the next channel block's halos at cb 3)
   bool nx_exists = false;
 
-  // One k-step: compile-time position Q in the tile's schedule (SCH): channel block CB, k-step
+  // One k-step: compile-time position Q in the tile's schedule (SCH): k-step
   // J of it, block BLK (0..15) and step TB within the block.
   auto step = [&](auto qc) __attribute__((always_inline)) {
     constexpr int Q = decltype(qc)::value;
-    constexpr int CB = SCH.cb[Q], J = SCH.j[Q], BLK = SCH.blk[Q], TB = SCH.t[Q];
+    constexpr int J = SCH.j[Q], BLK = SCH.blk[Q], TB = SCH.t[Q];
     constexpr int B8 = BLK % NBLK;
     constexpr int L = PB_LEN[BLK_PB[B8]], LPREV = PB_LEN[BLK_PB[(B8 + NBLK - 1) % NBLK]];
     constexpr bool BOUNDARY = TB == L - 1;  // the next k-step starts a new block

@@ -225,7 +225,9 @@ def test_kernel_selection_full_size(precision):
     assert kern["backbone.dla_down.projection_layer.0"].startswith("tv::stem::stem_conv<"), kern
     assert kern["backbone.dla_down.block_layers.0.conv1"].startswith("tv::c3s2::conv3x3s2<")
     assert kern["backbone.dla_down.block_layers.0.conv2+conv_residual"].startswith("tv::c3::conv3x3<")
-    assert ", 1, 4>" in kern["backbone.dla_down.block_layers.0.conv2+conv_residual"] or ", 1, 2>" in kern["backbone.dla_down.block_layers.0.conv2+conv_residual"]  # RES k-steps
+    # conv3x3<T, OutT, TW, ACT, EPI, RES, NI, SK>: the residual k-step variant
+    targs = kern["backbone.dla_down.block_layers.0.conv2+conv_residual"].split("<", 1)[1].rstrip(">").split(", ")
+    assert targs[5] == "1", kern["backbone.dla_down.block_layers.0.conv2+conv_residual"]
     assert kern["heads.*.0 (stacked) + LeakyReLU"].startswith("tv::c3::conv3x3<")
     assert kern["heads.*.2 (block-diagonal) -> fp32 NHWC"] == "(fused into the 3x3 heads)"
     assert kern["backbone.ida_up_reverse.upsample_layers.0+pad_to_match+add"].startswith("tv::convt::convt_add<")

@@ -37,6 +37,20 @@ MODEL_CASES = [
          in_h=480, in_w=640, batch=1, seed=105, objects=PLAIN4),
 ]
 
+# CenterpointDLA34 (centerpoint_dla.py:544-578; DLA-34 levels/channels fixed by dla34(),
+# :309-315) — SURVEY §8a a12-a15.
+DLA34_CASES = [
+    # small frames, batch 2, the plain 4-class heads [4, 2, 2]
+    dict(name="b2_64x96", in_h=64, in_w=96, batch=2, seed=200, objects=PLAIN4),
+    # 120x96: ceil-mode max-pool (15 -> 8 rows), pad_to_match crops (16 -> 15) and, in ida_up
+    # (f = 4: 32 -> 30 rows), the one-row downward shift; keypoint heads [4, 4, 8, 2, 2]
+    dict(name="b1_120x96_kp", in_h=120, in_w=96, batch=1, seed=201,
+         objects={"n_labels": 4, "keypoints_per_label": 1}),
+    # the BASELINE geometry (480x640) with the north-star DLA34 heads [4, 4, 8, 2, 2]
+    dict(name="b1_480x640_kp", in_h=480, in_w=640, batch=1, seed=202,
+         objects={"n_labels": 4, "keypoints_per_label": 1}),
+]
+
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 

@@ -57,3 +57,35 @@ def keypoint_owner(case):
         for slot in range(o.get("keypoints_per_label", 0)):
             owner.append((lab, slot))
     return owner
+
+
+# ---- CenterpointDLA34 cases (tests/golden/gen_golden_dla34.py) ----
+_DLA34 = None
+
+
+def dla34_index():
+    global _DLA34
+    if _DLA34 is None:
+        with open(os.path.join(GOLDEN, "models_dla34.json")) as f:
+            _DLA34 = json.load(f)
+    return _DLA34
+
+
+def dla34_state_dict(name):
+    """Seeded reference-layout weights (keys `model.*`), checked against the golden run's checksums."""
+    entry = dla34_index()[name]
+    sd = seeded_state_dict([(k, s) for k, s in entry["keys"]])
+    checks = golden(f"dla34_{name}")["weight_checksums"]
+    got = np.array([[float(v.double().sum()), float(v.double().abs().sum())]
+                    if v.dtype.is_floating_point else [float(v), 0.0] for v in sd.values()])
+    assert np.allclose(got, checks, rtol=1e-10, atol=1e-12), "seeded weight recipe drifted from the golden run"
+    return sd
+
+
+def dla34_input(name):
+    case = dla34_index()[name]["case"]
+    img = seeded_input(case)
+    chk = golden(f"dla34_{name}")["img_checksum"]
+    got = [float(img.double().sum()), float(img.double().abs().sum())]
+    assert np.allclose(got, chk, rtol=1e-10, atol=1e-9), "seeded input drifted from the golden run"
+    return img

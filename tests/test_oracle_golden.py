@@ -103,3 +103,58 @@ def test_forward_golden(name):
                     else:
                         row += [*d["keypoints"][j], d["keypoint_scores"][j], *d["keypoint_affinities"][j]]
                 np.testing.assert_array_equal(np.array(row, dtype=np.float64), ref[b, i])
+
+
+# ---- CenterpointDLA34 ----
+from helpers import dla34_index, dla34_state_dict, dla34_input  # noqa: E402
+from oracle.ref_dla34 import centerpoint_dla34_forward, deform_conv2d  # noqa: E402
+
+
+@pytest.mark.parametrize("name", list(dla34_index()))
+def test_dla34_forward_golden(name):
+    """Oracle == reference CenterpointDLA34 (with the DCNv2 restatement plugged in, see
+    gen_golden_dla34.py). Not bit-exact on every case: the reference's in-place `+=` and
+    torch's thread-split reductions differ at the last ulp, so 1e-6 relative."""
+    entry = dla34_index()[name]
+    case = entry["case"]
+    sd = {k[len("model."):]: v for k, v in dla34_state_dict(name).items()}
+    flags = dict(keypoints=case["objects"].get("keypoints_per_label", 0) > 0)
+    with torch.no_grad():
+        pred = centerpoint_dla34_forward(sd, dla34_input(name), flags, len(entry["head_channels"]))
+    g = golden(f"dla34_{name}")
+    for f in FIELDS:
+        t = getattr(pred, f)
+        if f in g.files:
+            ref = g[f]
+            np.testing.assert_allclose(t.contiguous().numpy(), ref, rtol=0, atol=1e-6 * max(1.0, np.abs(ref).max()),
+                                       err_msg=f)
+        else:
+            assert t is None
+
+
+def test_deform_conv2d_kat():
+    """Derived known answers for the DCNv2 restatement (parity otherwise unpinned): zero
+    offsets + unit mask == conv2d; a constant integer offset == conv2d of the shifted input
+    (interior pixels); mask scales each tap."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(2, 8, 13, 15, generator=g, dtype=torch.float64)
+    w = torch.randn(5, 8, 3, 3, generator=g, dtype=torch.float64)
+    b = torch.randn(5, generator=g, dtype=torch.float64)
+    off = torch.zeros(2, 18, 13, 15, dtype=torch.float64)
+    m = torch.ones(2, 9, 13, 15, dtype=torch.float64)
+    torch.testing.assert_close(deform_conv2d(x, off, m, w, b), F.conv2d(x, w, b, 1, 1), rtol=1e-12, atol=1e-12)
+    off[:, 0::2] = 1.0   # dy
+    off[:, 1::2] = -2.0  # dx
+    xs = torch.zeros_like(x)
+    xs[:, :, :-1, 2:] = x[:, :, 1:, :-2]
+    got = deform_conv2d(x, off, m, w, b)[:, :, 1:-2, 3:-1]
+    torch.testing.assert_close(got, F.conv2d(xs, w, b, 1, 1)[:, :, 1:-2, 3:-1], rtol=1e-12, atol=1e-12)
+    # half-pixel offset = mean of the two neighbours; mask 0.5 halves the tap
+    off.zero_()
+    off[:, 1::2] = 0.5
+    m.fill_(0.5)
+    xa = 0.5 * (x + torch.cat([x[:, :, :, 1:], torch.zeros_like(x[:, :, :, :1])], 3))
+    # (column 0 differs by design: its left tap samples x = -0.5, half of x[0], not padding)
+    torch.testing.assert_close(deform_conv2d(x, off, m, w, b)[..., 1:], F.conv2d(0.5 * xa, w, b, 1, 1)[..., 1:],
+                               rtol=1e-12, atol=1e-12)

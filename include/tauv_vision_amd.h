@@ -41,7 +41,13 @@ extern "C" {
 typedef enum tv_dtype { TV_F32 = 0, TV_F16 = 1, TV_BF16 = 2 } tv_dtype;
 
 /* Model description: the fields of ModelConfig (config.py:6-35) plus the head list of
- * get_head_channels() (centernet.py:114-142). */
+ * get_head_channels() (centernet.py:114-142). `arch` selects the network family:
+ * TV_ARCH_CENTERNET = Centernet(DLABackbone(heights, channels, downsamples)) (centernet.py:32-92,
+ * dla.py:393-416); TV_ARCH_DLA34 = CenterpointDLA34 (centerpoint_dla.py:544-578: DLA-34 base,
+ * DLAUp/IDAUp with DCNv2, down ratio 4, head_conv 256; n_levels/heights/channels/downsamples
+ * are ignored). */
+#define TV_ARCH_CENTERNET 0
+#define TV_ARCH_DLA34 1
 typedef struct tv_model_desc {
   int32_t n_levels;          /* len(backbone_heights) */
   int32_t heights[8];        /* backbone_heights */
@@ -51,6 +57,7 @@ typedef struct tv_model_desc {
   int32_t head_channels[16]; /* get_head_channels(object_config) */
   int32_t in_h, in_w;        /* ModelConfig.in_h / in_w */
   int32_t compute_dtype;     /* tv_dtype: TV_F32 = exact-f32 parity mode */
+  int32_t arch;              /* TV_ARCH_* */
 } tv_model_desc;
 
 typedef struct tv_engine tv_engine;

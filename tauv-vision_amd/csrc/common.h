@@ -161,6 +161,16 @@ int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad,
 int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cpad, int dtype,
                    hipStream_t s);
 // out[target] = add[target] for target pixels not covered by the shifted upsample.
+// CenterpointDLA34 bandwidth kernels (dla34.hip): NHWC, channels in whole 16-byte chunks.
+// MaxPool2d(2, 2, ceil_mode=True): out [B, ceil(H/2), ceil(W/2), C]
+int launch_maxpool2(const void* src, int B, int H, int W, int C, void* out, int Ho, int Wo, int dtype, hipStream_t s);
+// DCNv2 columns cols[pixel][tap][C] = sigmoid(om[18 + tap]) * bilinear(x, y + offset[2 tap], x + offset[2 tap + 1])
+int launch_dcn_sample(const void* x, int B, int H, int W, int C, const void* om, int om_ldc, void* cols, int dtype,
+                      hipStream_t s);
+// out = add + pad_to_match(depthwise ConvTranspose2d(src; weight fp32 [2f][2f][C], stride f, pad f/2)),
+// (sy, sx) = pad_to_match's (pad_above, pad_left)
+int launch_dwconvt_add(const void* src, int B, int h, int w, int C, const float* weight, int f, const void* add,
+                       int add_ldc, void* out, int tH, int tW, int sy, int sx, int dtype, hipStream_t s);
 int launch_uncovered_copy(const void* add, int add_ldc, void* out, int out_ldc, int C, int B,
                           int tH, int tW, int y0, int y1, int x0, int x1, int dtype,
                           hipStream_t s);

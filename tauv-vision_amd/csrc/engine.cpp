@@ -55,8 +55,16 @@ int Engine::fold(const std::string& conv, const std::string& bn, int cout, std::
                  std::vector<double>& shift) {
   scale.assign(cout, 1.0);
   shift.assign(cout, 0.0);
-  const float* b = weight(conv + ".bias", cout);
-  if (!b) return TV_ENOTFOUND;
+  // bias=False convs (DLA34, centerpoint_dla.py:24-27) have no `.bias` key in the layout
+  std::vector<float> zeros;
+  const float* b = nullptr;
+  if (plan.names.count(conv + ".bias")) {
+    b = weight(conv + ".bias", cout);
+    if (!b) return TV_ENOTFOUND;
+  } else {
+    zeros.assign(cout, 0.f);
+    b = zeros.data();
+  }
   for (int i = 0; i < cout; ++i) shift[i] = b[i];
   if (bn.empty()) return TV_OK;
   const float* g = weight(bn + ".weight", cout);
@@ -77,7 +85,19 @@ int Engine::pack_op(size_t oi) {
   Packed& pk = packed[oi];
   const int esz = dtype_size(dtype);
   const int BK = 128 / esz;
-  if (op.kind == OP_PREP) return TV_OK;
+  if (op.kind == OP_PREP || op.kind == OP_MAXPOOL || op.kind == OP_DCN) return TV_OK;
+  if (op.kind == OP_DWCONVT_ADD) {  // depthwise ConvTranspose2d weight [C][1][2f][2f] -> fp32 [2f][2f][C]
+    const int c = op.N, k = 2 * op.up_s;
+    const float* w = weight(op.up_w + ".weight", (int64_t)c * k * k);
+    if (!w) return TV_ENOTFOUND;
+    std::vector<float> t((size_t)k * k * c);
+    for (int co = 0; co < c; ++co)
+      for (int tap = 0; tap < k * k; ++tap) t[(size_t)tap * c + co] = w[(size_t)co * k * k + tap];
+    TV_HIP(hipMalloc(&pk.w, t.size() * sizeof(float)));
+    TV_HIP(hipMemcpy(pk.w, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+    weight_bytes += t.size() * sizeof(float);
+    return TV_OK;
+  }
 
   std::vector<float> hw;    // [Npad][Kpad] fp32 staging
   std::vector<float> bias;  // [Npad]
@@ -144,6 +164,11 @@ int Engine::pack_op(size_t oi) {
       for (size_t si = 0; si < op.segs.size(); ++si) {
         const SegSpec& sg = op.segs[si];
         const int cs = plan.tensors[sg.src].C;
+        if (sg.identity) {  // residual added as-is: identity 1x1 (exact in every compute dtype)
+          for (int co = 0; co < std::min(N, sg.cin); ++co) hw[(size_t)co * pk.Kpad + (size_t)kb * BK + co] = 1.f;
+          kb += pk.seg_ksteps[si];
+          continue;
+        }
         // total input channels of the PyTorch weight = max over segments sharing it
         int wcin = 0;
         for (const SegSpec& o : op.segs)
@@ -312,7 +337,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
     const OpSpec& op = plan.ops[i];
     if (op.out >= 0) def[op.out] = (int)i, last[op.out] = std::max(last[op.out], (int)i);
     for (const SegSpec& s : op.segs) last[s.src] = std::max(last[s.src], (int)i);
-    if (op.kind == OP_CONVT_ADD) last[op.src] = std::max(last[op.src], (int)i);
+    if (op.src >= 0) last[op.src] = std::max(last[op.src], (int)i);
     if (op.add >= 0) last[op.add] = std::max(last[op.add], (int)i);
   }
   ws->off.assign(nt, 0);
@@ -344,7 +369,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   char* base = (char*)ws->arena;
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
-    if (op.kind == OP_PREP) continue;
+    if (op.kind != OP_CONV && op.kind != OP_CONVT_ADD) continue;  // DLA34 bandwidth ops: no GEMM
     ConvParams& p = ws->params[i];
     const Packed& pk = packed[i];
     std::memset(&p, 0, sizeof(p));
@@ -410,7 +435,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->c3_ni.assign(plan.ops.size(), 4);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
-    if (op.kind == OP_PREP) continue;
+    if (op.kind != OP_CONV && op.kind != OP_CONVT_ADD) continue;
     ConvParams& p = ws->params[i];
     std::vector<KStep> ks;
     bool ok = true;
@@ -671,6 +696,18 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     return input_u8 ? launch_prep_u8((const uint8_t*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s)
                     : launch_prep_nchw((const float*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s);
   }
+  if (op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_DWCONVT_ADD) {
+    const TensorSpec& src = plan.tensors[op.src];
+    const TensorSpec& dst = plan.tensors[op.out];
+    void* o = base + ws->off[op.out];
+    const void* x = base + ws->off[op.src];
+    if (op.kind == OP_MAXPOOL) return launch_maxpool2(x, ws->B, src.H, src.W, src.C, o, dst.H, dst.W, dtype, s);
+    const TensorSpec& ad = plan.tensors[op.add];
+    const void* a = base + ws->off[op.add];
+    if (op.kind == OP_DCN) return launch_dcn_sample(x, ws->B, src.H, src.W, src.C, a, ad.C, o, dtype, s);
+    return launch_dwconvt_add(x, ws->B, src.H, src.W, src.C, (const float*)packed[i].w, op.up_s, a, ad.C, o, dst.H,
+                              dst.W, op.sy, op.sx, dtype, s);
+  }
   if (ws->head_skip[i]) return TV_OK;  // fused into the 3x3 heads launch
   if (ws->head_fused[i]) {
     TV_HIP(hipMemsetAsync(out, 0, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad * sizeof(float), s));
@@ -819,6 +856,10 @@ const char* Engine::op_kernel(int B, size_t i) {
     const char* t = tn[dtype];
     const char* o = (op.out < 0) ? "float" : t;
     std::string& name = ws->kname[i];
+    if (name.empty() && (op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_DWCONVT_ADD))
+      name = std::string(op.kind == OP_MAXPOOL ? "tv::dla::maxpool2_ceil<" : op.kind == OP_DCN ? "tv::dla::dcn_sample<"
+                                                                                            : "tv::dla::dwconvt_add<") +
+             t + ">";
     if (name.empty()) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";

@@ -300,6 +300,11 @@ struct Walker {
 }  // namespace
 
 int build_plan(const tv_model_desc& d, Plan* plan) {
+  if (d.arch == TV_ARCH_DLA34) return build_plan_dla34(d, plan);
+  if (d.arch != TV_ARCH_CENTERNET) {
+    set_error("unknown model arch");
+    return TV_EINVAL;
+  }
   if (d.n_levels < 1 || d.n_levels > 8 || d.downsamples < 0 || d.downsamples > 6 || d.n_heads < 1 ||
       d.n_heads > 16 || d.in_h < 1 || d.in_w < 1 || d.compute_dtype < 0 || d.compute_dtype > 2) {
     set_error("model desc out of range");
@@ -325,6 +330,7 @@ int build_plan(const tv_model_desc& d, Plan* plan) {
   *plan = Plan();
   Walker w(d, *plan);
   w.params();
+  for (const ParamInfo& p : plan->params) plan->names.insert(p.name);
   int rc = w.forward();
   if (rc) return rc;
   for (auto& op : plan->ops)

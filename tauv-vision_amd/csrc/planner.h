@@ -3,6 +3,7 @@
 // fused GEMM launches over NHWC tensors.
 #pragma once
 #include <cstdint>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -25,9 +26,21 @@ struct SegSpec {
   int kh, kw, stride, pad;
   int pad_w = -1;        // width padding when it differs from `pad` (row-expanded stem input)
   int row_expand = 0;    // k > 0: `src` holds the k horizontal taps of a k x k conv per pixel
+                         // (DCN columns: k = 9 taps of a 3x3 weight per pixel, kh = kw = 1)
+  bool identity = false; // residual added as-is (BasicBlock residual = x): an identity 1x1 weight
 };
 
-enum OpKind { OP_PREP = 0, OP_CONV = 1, OP_CONVT_ADD = 2 };
+enum OpKind {
+  OP_PREP = 0,
+  OP_CONV = 1,
+  OP_CONVT_ADD = 2,
+  // CenterpointDLA34 (centerpoint_dla.py): elementwise / gather ops on HBM bandwidth
+  OP_MAXPOOL = 3,    // MaxPool2d(2, 2, ceil_mode=True) of `src` (Tree.downsample, :199-200)
+  OP_DCN = 4,        // DCNv2 sampling: columns [9 taps][C] per pixel of `src` at the offsets /
+                     // sigmoid(mask logits) in tensor `add` (18 offsets, 9 logits; :386-392)
+  OP_DWCONVT_ADD = 5 // depthwise ConvTranspose2d(2f, f, f//2) of `src` + pad_to_match + `add`
+                     // (IDAUp, :446-451); up_s = f, (sy, sx) = (pad_above, pad_left)
+};
 
 struct OpSpec {
   int kind;
@@ -60,9 +73,11 @@ struct Plan {
   int out_h = 0, out_w = 0, out_c = 0, out_cpad = 0;
   int in_cpad = 0;
   double flops_per_frame = 0;
+  std::set<std::string> names;       // every key of `params`
 };
 
 // Returns 0 or a TV_E* code (with tv_last_error set).
 int build_plan(const tv_model_desc& d, Plan* plan);
+int build_plan_dla34(const tv_model_desc& d, Plan* plan);  // planner_dla34.cpp
 
 }  // namespace tv

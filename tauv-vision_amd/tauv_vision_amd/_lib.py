@@ -20,7 +20,7 @@ c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_floa
 class ModelDesc(ctypes.Structure):
     _fields_ = [("n_levels", c_i32), ("heights", c_i32 * 8), ("channels", c_i32 * 9), ("downsamples", c_i32),
                 ("n_heads", c_i32), ("head_channels", c_i32 * 16), ("in_h", c_i32), ("in_w", c_i32),
-                ("compute_dtype", c_i32)]
+                ("compute_dtype", c_i32), ("arch", c_i32)]
 
 
 class WeightView(ctypes.Structure):

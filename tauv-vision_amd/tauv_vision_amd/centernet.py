@@ -17,7 +17,7 @@ from . import _lib
 from .config import ObjectConfigSet
 from .dla import DLABackbone, populate
 from .engine import NativeEngine
-from .weights import model_desc, param_layout
+from .weights import model_desc, dla34_desc, param_layout
 
 
 @dataclass
@@ -83,22 +83,16 @@ def prediction_from_nhwc(out: torch.Tensor, object_config: ObjectConfigSet) -> P
     return Prediction(**fields)
 
 
-class Centernet(nn.Module):
-    """centernet.py:32-92. `precision`: "fp32" (exact-f32 MFMA, parity mode), "fp16" or
-    "bf16" (fp32 accumulation; throughput mode)."""
+class _NativeModel(nn.Module):
+    """Engine cache + the reference forward API shared by Centernet and CenterpointDLA34.
+    Subclasses provide `_desc(in_h, in_w)` (the native model description) and `_key()`."""
 
-    def __init__(self, backbone: DLABackbone, object_config: ObjectConfigSet, precision: str = "fp32"):
-        super().__init__()
-        self.backbone = backbone
+    def _init_native(self, object_config, precision):
         self.object_config = object_config
         self.head_channels = get_head_channels(object_config)
         if precision not in _lib.DTYPES:
             raise ValueError(f"precision must be one of {sorted(_lib.DTYPES)}")
         self.precision = precision
-        desc = model_desc(backbone.heights, backbone.channels, backbone.downsamples, self.head_channels)
-        layout = [(k, s) for k, s in param_layout(desc) if k.startswith("heads.")]
-        self.heads = nn.Module()
-        populate(self.heads, [(k[len("heads."):], s) for k, s in layout], seed_layout=layout, prefix="heads.")
         self._version = [0]
         self._engines = {}
         self.register_load_state_dict_post_hook(lambda module, keys: module.invalidate())
@@ -120,6 +114,9 @@ class Centernet(nn.Module):
         self.invalidate()
         return self
 
+    def _key(self):
+        return (self._version[0],)
+
     def _device_for(self, t: torch.Tensor) -> torch.device:
         if not torch.cuda.is_available():
             raise RuntimeError("tauv_vision_amd needs a gfx950 (MI355X) GPU; no HIP device is visible")
@@ -130,12 +127,10 @@ class Centernet(nn.Module):
 
     def engine(self, device: torch.device, in_h: int, in_w: int) -> NativeEngine:
         key = (device.index if device.index is not None else torch.cuda.current_device(), in_h, in_w,
-               self.precision, self._version[0], self.backbone._version[0])
+               self.precision) + self._key()
         eng = self._engines.get(key)
         if eng is None:
-            desc = model_desc(self.backbone.heights, self.backbone.channels, self.backbone.downsamples,
-                              self.head_channels, in_h, in_w, self.precision)
-            eng = NativeEngine(desc, self.state_dict(), key[0])
+            eng = NativeEngine(self._desc(in_h, in_w), self.state_dict(), key[0])
             self._engines = {key: eng}
         return eng
 
@@ -166,6 +161,46 @@ class Centernet(nn.Module):
         return decode(self.forward_frames(frames), model_config, n_detections, score_threshold)
 
 
+class Centernet(_NativeModel):
+    """centernet.py:32-92. `precision`: "fp32" (exact-f32 MFMA, parity mode), "fp16" or
+    "bf16" (fp32 accumulation; throughput mode)."""
+
+    def __init__(self, backbone: DLABackbone, object_config: ObjectConfigSet, precision: str = "fp32"):
+        super().__init__()
+        self.backbone = backbone
+        self._init_native(object_config, precision)
+        desc = model_desc(backbone.heights, backbone.channels, backbone.downsamples, self.head_channels)
+        layout = [(k, s) for k, s in param_layout(desc) if k.startswith("heads.")]
+        self.heads = nn.Module()
+        populate(self.heads, [(k[len("heads."):], s) for k, s in layout], seed_layout=layout, prefix="heads.")
+
+    def _key(self):
+        return (self._version[0], self.backbone._version[0])
+
+    def _desc(self, in_h, in_w):
+        return model_desc(self.backbone.heights, self.backbone.channels, self.backbone.downsamples,
+                          self.head_channels, in_h, in_w, self.precision)
+
+
+class CenterpointDLA34(_NativeModel):
+    """centerpoint_dla.py:544-578: DLASeg('dla34', heads {'0'..'n-1'}, down_ratio 4,
+    final_kernel 1, last_level 5, head_conv 256) under `self.model`, so reference checkpoints
+    (keys `model.base...`, `model.dla_up...`, `model.ida_up...`, `model.<i>.{0,2}...`) load
+    unchanged. The reference constructor downloads ImageNet DLA-34 weights (get_pose_net,
+    :534-541); here the parameters start from the seeded recipe and a checkpoint is loaded
+    with load_state_dict. DCNv2 runs natively (csrc/dla34.hip + MFMA GEMM over its columns)."""
+
+    def __init__(self, object_config: ObjectConfigSet, precision: str = "fp32"):
+        super().__init__()
+        self._init_native(object_config, precision)
+        layout = param_layout(dla34_desc(self.head_channels))
+        self.model = nn.Module()
+        populate(self.model, [(k[len("model."):], s) for k, s in layout], seed_layout=layout, prefix="model.")
+
+    def _desc(self, in_h, in_w):
+        return dla34_desc(self.head_channels, in_h, in_w, self.precision)
+
+
 def initialize_weights(module: nn.Module, excluded_modules=()):
     """centernet.py:103-111 analogue: re-draw every conv/conv-transpose weight xavier-uniform
     and zero its bias (parameter tree leaves with a 4-D weight)."""
@@ -181,5 +216,5 @@ def initialize_weights(module: nn.Module, excluded_modules=()):
                 if b is not None:
                     b.zero_()
     for m in module.modules():
-        if isinstance(m, Centernet):
+        if isinstance(m, _NativeModel):
             m.invalidate()

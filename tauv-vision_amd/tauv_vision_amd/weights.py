@@ -8,7 +8,11 @@ import torch
 from . import _lib
 
 
-def model_desc(heights, channels, downsamples, head_channels, in_h=64, in_w=64, precision="fp32"):
+ARCH_CENTERNET, ARCH_DLA34 = 0, 1
+
+
+def model_desc(heights, channels, downsamples, head_channels, in_h=64, in_w=64, precision="fp32",
+               arch=ARCH_CENTERNET):
     if len(channels) != len(heights) + 1:
         raise ValueError("backbone_channels must have len(backbone_heights) + 1 entries")
     if len(heights) > 8 or len(head_channels) > 16:
@@ -27,7 +31,13 @@ def model_desc(heights, channels, downsamples, head_channels, in_h=64, in_w=64, 
     if precision not in _lib.DTYPES:
         raise ValueError(f"precision must be one of {sorted(_lib.DTYPES)}")
     d.compute_dtype = _lib.DTYPES[precision]
+    d.arch = int(arch)
     return d
+
+
+def dla34_desc(head_channels, in_h=64, in_w=64, precision="fp32"):
+    """CenterpointDLA34 (centerpoint_dla.py:544-578): the DLA-34 structure is fixed."""
+    return model_desc([], [16], 2, head_channels, in_h, in_w, precision, arch=ARCH_DLA34)
 
 
 def param_layout(desc):

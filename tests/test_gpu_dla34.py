@@ -1,0 +1,96 @@
+"""GPU parity of the native CenterpointDLA34 forward against goldens
+made by the reference module (tests/golden/gen_golden_dla34.py; DCNv2 = the oracle's
+torchvision restatement, parity unpinned for that function only).
+
+fp32 (exact-f32 MFMA, BN folded): every Prediction tensor within 1e-4 * max(1, |ref|max).
+fp16 / bf16 (throughput modes): 3e-2 / 1.5e-1 of the tensor's range — DCN offsets are
+produced in the compute dtype, so sampling positions carry its rounding.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import golden, dla34_index, dla34_state_dict, dla34_input
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ["heatmap", "keypoint_heatmap", "keypoint_affinity", "size", "offset", "roll_bin", "roll_offset",
+          "pitch_bin", "pitch_offset", "yaw_bin", "yaw_offset", "depth"]
+TOL = {"fp32": 1e-4, "fp16": 3e-2, "bf16": 1.5e-1}
+
+
+def build(name, precision):
+    import tauv_vision_amd as tv
+    case = dla34_index()[name]["case"]
+    o = case["objects"]
+    A = tv.AngleConfig
+    kp = o.get("keypoints_per_label", 0)
+    cfgs = [tv.ObjectConfig(f"o{i}", A(False, 1.0), A(False, 1.0), A(False, 1.0), False, kp > 0,
+                            [(0.0, 0.0, 0.0)] * kp if kp else None) for i in range(o["n_labels"])]
+    oc = tv.ObjectConfigSet(cfgs)
+    model = tv.CenterpointDLA34(oc, precision=precision)
+    model.load_state_dict(dla34_state_dict(name))
+    model = model.cuda().eval()
+    mc = tv.ModelConfig([], [], case["in_h"], case["in_w"], 2, 1.0)
+    return model, oc, mc, case
+
+
+def _cmp(pred, g, tol):
+    for f in FIELDS:
+        t = getattr(pred, f)
+        if f not in g.files:
+            assert t is None, f
+            continue
+        ref = g[f]
+        got = t.detach().cpu().numpy()
+        assert got.shape == ref.shape, (f, got.shape, ref.shape)
+        scale = max(1.0, float(np.abs(ref).max()))
+        err = float(np.abs(got - ref).max())
+        assert err <= tol * scale, f"{f}: max|err| {err:.3e} > {tol} * {scale:.3g}"
+
+
+@pytest.mark.parametrize("name", list(dla34_index()))
+def test_dla34_fp32_matches_reference(name):
+    model, oc, mc, case = build(name, "fp32")
+    with torch.no_grad():
+        pred = model(dla34_input(name).cuda())
+    g = golden(f"dla34_{name}")
+    _cmp(pred, g, TOL["fp32"])
+    import tauv_vision_amd as tv
+    for thr in (0.05, 0.3):  # end-to-end decode on the network output
+        got = tv.decode(pred, mc, 20, thr)
+        ref = g[f"decode_thr{thr}"]
+        for b in range(ref.shape[0]):
+            assert len(got[b]) == int(np.nansum(ref[b, :, 7]))
+            for i, d in enumerate(got[b]):
+                assert int(d.label) == int(ref[b, i, 0])
+                np.testing.assert_allclose([float(d.score), d.y, d.x, d.h, d.w], ref[b, i, 1:6], atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("name", list(dla34_index()))
+def test_dla34_low_precision(name, precision):
+    model, oc, mc, case = build(name, precision)
+    with torch.no_grad():
+        pred = model(dla34_input(name).cuda())
+    _cmp(pred, golden(f"dla34_{name}"), TOL[precision])
+
+
+def test_dla34_u8_frames_and_batch_independence():
+    """forward_frames (fused ToTensor+Normalize) == forward on the normalised input, and a
+    frame's output does not depend on its batch neighbours (B=3 vs B=1 slices)."""
+    import tauv_vision_amd as tv
+    name = "b2_64x96"
+    model, oc, mc, case = build(name, "fp16")
+    g = torch.Generator().manual_seed(5)
+    u8 = torch.randint(0, 256, (3, case["in_h"], case["in_w"], 3), generator=g, dtype=torch.uint8)
+    mean = torch.tensor([0.485, 0.456, 0.406]).view(1, 3, 1, 1)
+    std = torch.tensor([0.229, 0.224, 0.225]).view(1, 3, 1, 1)
+    img = (u8.permute(0, 3, 1, 2).float() / 255.0 - mean) / std
+    with torch.no_grad():
+        a = model.forward_frames(u8.cuda()).heatmap.float().cpu()
+        b = model(img.cuda()).heatmap.float().cpu()
+        c = model(img[1:2].cuda()).heatmap.float().cpu()
+    scale = max(1.0, float(b.abs().max()))
+    assert float((a - b).abs().max()) <= 2e-2 * scale
+    assert float((b[1:2] - c).abs().max()) <= 1e-3 * scale

@@ -140,3 +140,30 @@ def test_seeded_recipe_matches_golden_recipe():
     b = seeded_state_dict(keys)
     for k in a:
         assert torch.equal(a[k], b[k]), k
+
+
+def test_dla34_param_layout_matches_reference_keys():
+    """The native planner's CenterpointDLA34 state_dict layout == the reference module's
+    (keys, shapes, order), for both head sets of the goldens; no GPU needed."""
+    from helpers import dla34_index
+    from tauv_vision_amd.weights import dla34_desc, param_layout, geometry
+    for name, e in dla34_index().items():
+        d = dla34_desc(e["head_channels"], e["case"]["in_h"], e["case"]["in_w"])
+        assert param_layout(d) == [(k, tuple(s)) for k, s in e["keys"]], name
+        geo = geometry(d)
+        assert (geo["out_h"], geo["out_w"]) == (e["case"]["in_h"] // 4, e["case"]["in_w"] // 4)
+        assert geo["out_channels"] == sum(e["head_channels"])
+
+
+def test_dla34_module_state_dict_loads_reference_checkpoint_keys():
+    import tauv_vision_amd as tv
+    from helpers import dla34_index, dla34_state_dict
+    name = "b2_64x96"
+    oc = tv.ObjectConfigSet([tv.ObjectConfig(f"o{i}", tv.AngleConfig(False, 1.0), tv.AngleConfig(False, 1.0),
+                                             tv.AngleConfig(False, 1.0), False, False, None) for i in range(4)])
+    m = tv.CenterpointDLA34(oc)
+    sd = dla34_state_dict(name)
+    assert list(m.state_dict().keys()) == list(sd.keys())
+    m.load_state_dict(sd)  # strict
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 64, 96)) if not torch.cuda.is_available() else (_ for _ in ()).throw(RuntimeError())

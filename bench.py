@@ -36,11 +36,16 @@ PEAK_TFLOPS = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.3}  # dense MFMA, MI3
 METRIC = "frames/sec CenterNet-R18 640x480 batch=1 & 64; 1/2/4/8 MI355X + %roofline"
 
 
-def build_model(precision, device):
+def build_model(precision, device, arch="r18"):
     A = tv.AngleConfig
-    oc = tv.ObjectConfigSet([tv.ObjectConfig(f"class{i}", A(False, None), A(False, None), A(False, None), False,
-                                             False, None) for i in range(N_LABELS)])
-    model = tv.Centernet(tv.DLABackbone(HEIGHTS, CHANNELS, DOWNSAMPLES), oc, precision=precision)
+    if arch == "dla34":  # DLA34 with the keypoint heads [4, 4, 8, 2, 2]
+        oc = tv.ObjectConfigSet([tv.ObjectConfig(f"class{i}", A(False, None), A(False, None), A(False, None), False,
+                                                 True, [(0.0, 0.0, 0.0)]) for i in range(N_LABELS)])
+        model = tv.CenterpointDLA34(oc, precision=precision)
+    else:
+        oc = tv.ObjectConfigSet([tv.ObjectConfig(f"class{i}", A(False, None), A(False, None), A(False, None), False,
+                                                 False, None) for i in range(N_LABELS)])
+        model = tv.Centernet(tv.DLABackbone(HEIGHTS, CHANNELS, DOWNSAMPLES), oc, precision=precision)
     sd = seeded_state_dict([(k, tuple(v.shape)) for k, v in model.state_dict().items()])
     model.load_state_dict(sd)
     return model.to(device).eval(), oc, sd
@@ -133,7 +138,7 @@ def conv_roofline(pipe, frames, precision, reps=3):
                               "tflops": round(o[2] / max(o[1], 1e-9) / 1e9, 1)} for o in top]}
 
 
-def cpu_baseline(sd, seconds, K, thr):
+def cpu_baseline(sd, seconds, K, thr, arch="r18"):
     """The repo's PyTorch-CPU restatement of the reference path (oracle/), fp32, timed on a
     bounded sample of single 640x480 frames (forward + decode) on this host's cores."""
     sys.path.insert(0, ROOT)
@@ -148,7 +153,12 @@ def cpu_baseline(sd, seconds, K, thr):
         while True:
             u8 = torch.randint(0, 256, (1, 480, 640, 3), generator=g, dtype=torch.uint8)
             img = normalize(u8.permute(0, 3, 1, 2).float() / 255.0)
-            pred = oracle.centernet_forward(sd, img, HEIGHTS, DOWNSAMPLES, {})
+            if arch == "dla34":
+                from oracle.ref_dla34 import centerpoint_dla34_forward
+                pred = centerpoint_dla34_forward({k[len("model."):]: v for k, v in sd.items()}, img,
+                                                 {"keypoints": True}, 5)
+            else:
+                pred = oracle.centernet_forward(sd, img, HEIGHTS, DOWNSAMPLES, {})
             oracle.decode(pred, 480, 640, DOWNSAMPLES, K, thr)
             n += 1
             el = time.perf_counter() - t0
@@ -172,6 +182,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-b1", action="store_true")
     ap.add_argument("--b1-steps", type=int, default=200)
+    ap.add_argument("--model", default="r18", choices=["r18", "dla34"],
+                    help="r18: the BASELINE CenterNet-R18 (headline); dla34: CenterpointDLA34, heads [4,4,8,2,2]")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -183,7 +195,7 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     H, W, B, K = 480, 640, args.batch, args.k
-    model, oc, sd = build_model(args.precision, device)
+    model, oc, sd = build_model(args.precision, device, args.model)
     mc = tv.ModelConfig(HEIGHTS, CHANNELS, H, W, DOWNSAMPLES, 1.0)
     gen = torch.Generator(device=device).manual_seed(1000 + rank)
     frames = torch.randint(0, 256, (B, H, W, 3), generator=gen, device=device, dtype=torch.uint8)
@@ -242,15 +254,16 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, args.cpu_seconds, K, args.thr)
+        cpu = cpu_baseline({k: v.detach().cpu() for k, v in sd.items()}, args.cpu_seconds, K, args.thr, args.model)
 
     if rank == 0:
+        workload = (f"CenterNet-R18 (Centernet+DLABackbone [2]*5/[128]*6, ds 2, heads [4,2,2]) " if args.model == "r18"
+                    else "CenterpointDLA34 (DLA-34 + DLAUp/IDAUp with DCNv2, heads [4,4,8,2,2]) ")
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "frames/sec", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC if args.model == "r18" else METRIC.replace("CenterNet-R18", "CenterpointDLA34"), "value": round(value, 2), "unit": "frames/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
-            "config": {"workload": f"CenterNet-R18 (Centernet+DLABackbone [2]*5/[128]*6, ds 2, heads [4,2,2]) "
-                                   f"640x480 u8 frames, batch={B}/GPU, forward + decode(K={K}, thr={args.thr})",
+            "config": {"workload": workload + f"640x480 u8 frames, batch={B}/GPU, forward + decode(K={K}, thr={args.thr})",
                        "global_batch": B * world, "parallelism": f"dp{world} (frame-sharded, RCCL all-gather of "
                                                                   f"detections)" if world > 1 else "dp1"},
             "e2e_tflops": round(value * flops_frame / 1e12, 2),

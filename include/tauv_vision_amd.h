@@ -139,6 +139,23 @@ int tv_decode(const float* heat, const int64_t heat_strides[4], const float* siz
               const float* aux, const int64_t aux_strides[5], float* records, int32_t* counts, void* workspace,
               int64_t workspace_bytes, void* stream);
 
+/* YOLACT post-processing (reference src/tauv_vision/yolact/model/), fp32,
+ * device pointers, async on `stream`.
+ * box_decode (boxes.py:55-61): enc [B,A,4] (y, x, h, w encodings), anchor [anchor_batch,A,4]
+ *   (anchor_batch 1 broadcasts like the reference's [1,A,4] anchors), out [B,A,4]. */
+int tv_yolact_box_decode(const float* box_encoding, const float* anchor, int32_t B, int32_t A, int32_t anchor_batch,
+                         float variance0, float variance1, float* box, void* stream);
+/* nms (nms.py:7-29): class-agnostic fast NMS of batch 0 — classification [A, C+1] logits and
+ * box [A, 4] of batch 0; writes the kept anchor indices (descending confidence) to det[<= top_k]
+ * (int64) and their number to *n_det (device int32). A <= 8192. */
+int tv_yolact_fast_nms(const float* classification, int32_t A, int32_t n_classes_with_bg, const float* box,
+                       int32_t top_k, float iou_threshold, float confidence_threshold, int64_t* det, int32_t* n_det,
+                       void* stream);
+/* assemble_mask (masks.py:8-21): prototypes [K,H,W], coefficients [n,K], box [n,4] (y, x, h, w
+ * normalised) or NULL -> mask [n,H,W] = sigmoid(coeff . proto) x inclusive box mask. */
+int tv_yolact_assemble_mask(const float* mask_prototype, int32_t K, int32_t H, int32_t W, const float* mask_coeff,
+                            const float* box, int32_t n, float* mask, void* stream);
+
 const char* tv_last_error(void);
 const char* tv_version(void);
 

@@ -185,6 +185,32 @@ int tv_index_split(const int32_t* flat, int32_t B, int32_t K, int32_t H, int32_t
   })
 }
 
+int tv_yolact_box_decode(const float* enc, const float* anchor, int32_t B, int32_t A, int32_t anchor_batch, float v0,
+                         float v1, float* box, void* stream) {
+  TV_GUARD({
+    if (!enc || !anchor || !box) { set_error("bad argument"); return TV_EINVAL; }
+    return launch_yolact_box_decode(enc, anchor, B, A, anchor_batch, v0, v1, box, (hipStream_t)stream);
+  })
+}
+
+int tv_yolact_fast_nms(const float* cls, int32_t A, int32_t C1, const float* box, int32_t top_k, float iou_thr,
+                       float conf_thr, int64_t* det, int32_t* n_det, void* stream) {
+  TV_GUARD({
+    if (!cls || !box || !det || !n_det) { set_error("bad argument"); return TV_EINVAL; }
+    return launch_yolact_fast_nms(cls, A, C1, box, top_k, iou_thr, conf_thr, (long long*)det, n_det,
+                                  (hipStream_t)stream);
+  })
+}
+
+int tv_yolact_assemble_mask(const float* proto, int32_t K, int32_t H, int32_t W, const float* coeff, const float* box,
+                            int32_t n, float* mask, void* stream) {
+  TV_GUARD({
+    if (n == 0) return TV_OK;
+    if (!proto || !coeff || !mask) { set_error("bad argument"); return TV_EINVAL; }
+    return launch_yolact_assemble_mask(proto, K, H, W, coeff, box, n, mask, (hipStream_t)stream);
+  })
+}
+
 int tv_decode_workspace_size(int32_t B, int32_t C, int32_t H, int32_t W, int32_t K, int64_t* bytes) {
   if (!bytes || B < 1 || C < 1 || H < 1 || W < 1 || K < 1) { set_error("bad argument"); return TV_EINVAL; }
   int64_t peaks = ((int64_t)B * C * H * W * 4 + 255) / 256 * 256;

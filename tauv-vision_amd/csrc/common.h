@@ -171,6 +171,14 @@ int launch_dcn_sample(const void* x, int B, int H, int W, int C, const void* om,
 // (sy, sx) = pad_to_match's (pad_above, pad_left)
 int launch_dwconvt_add(const void* src, int B, int h, int w, int C, const float* weight, int f, const void* add,
                        int add_ldc, void* out, int tH, int tW, int sy, int sx, int dtype, hipStream_t s);
+// YOLACT post-processing (yolact.hip), fp32: box_decode (boxes.py:55-61), batch-0 fast NMS
+// (nms.py:7-29; det = kept anchor indices in descending-confidence order), assemble_mask (masks.py:8-21)
+int launch_yolact_box_decode(const float* enc, const float* anchor, int B, int A, int anchor_batch, float v0, float v1,
+                             float* out, hipStream_t s);
+int launch_yolact_fast_nms(const float* cls, int A, int C1, const float* box, int top_k, float iou_thr, float conf_thr,
+                           long long* det, int* n_det, hipStream_t s);
+int launch_yolact_assemble_mask(const float* proto, int K, int H, int W, const float* coeff, const float* box, int n,
+                                float* out, hipStream_t s);
 int launch_uncovered_copy(const void* add, int add_ldc, void* out, int out_ldc, int C, int B,
                           int tH, int tW, int y0, int y1, int x0, int x1, int dtype,
                           hipStream_t s);

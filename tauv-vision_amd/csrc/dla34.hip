@@ -42,13 +42,17 @@ __global__ __launch_bounds__(256) void maxpool2_ceil(const T* __restrict__ src, 
                                                      T* __restrict__ out, int Ho, int Wo) {
   constexpr int V = Vec<T>::N;
   const int nq = C / V;
-  const long total = (long)B * Ho * Wo * nq;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % nq);
-    const long pix = i / nq;
-    const int ox = (int)(pix % Wo);
-    const int oy = (int)((pix / Wo) % Ho);
-    const int b = (int)(pix / ((long)Wo * Ho));
+  const unsigned total = (unsigned)B * Ho * Wo * nq;  // < 2^31 (checked by the launcher)
+  {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    // 32-bit index math: 64-bit division is a long software sequence on CDNA
+    const unsigned q = i % (unsigned)nq;
+    const unsigned pix = i / (unsigned)nq;
+    const unsigned ox = pix % (unsigned)Wo;
+    const unsigned r = pix / (unsigned)Wo;
+    const unsigned oy = r % (unsigned)Ho;
+    const unsigned b = r / (unsigned)Ho;
     Vec<T> m;
 #pragma unroll
     for (int e = 0; e < V; ++e) m.v[e] = -__builtin_inff();
@@ -59,12 +63,12 @@ __global__ __launch_bounds__(256) void maxpool2_ceil(const T* __restrict__ src, 
         const int y = 2 * oy + dy, x = 2 * ox + dx;
         if (y < H && x < W) {  // ceil mode: the last window may hang over the edge
           Vec<T> t;
-          load_vec(src + (((long)b * H + y) * W + x) * C + q * V, t);
+          load_vec(src + (((size_t)b * H + y) * W + x) * C + q * V, t);
 #pragma unroll
           for (int e = 0; e < V; ++e) m.v[e] = fmaxf(m.v[e], t.v[e]);
         }
       }
-    store_vec(out + pix * C + q * V, m);
+    store_vec(out + (size_t)pix * C + q * V, m);
   }
 }
 
@@ -75,16 +79,19 @@ __global__ __launch_bounds__(256) void dcn_sample(const T* __restrict__ x, int B
                                                   const T* __restrict__ om, int om_ldc, T* __restrict__ cols) {
   constexpr int V = Vec<T>::N;
   const int nq = C / V;
-  const long total = (long)B * H * W * 9 * nq;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % nq);
-    const long r = i / nq;
-    const int k = (int)(r % 9);
-    const long pix = r / 9;
-    const int ox = (int)(pix % W);
-    const int oy = (int)((pix / W) % H);
-    const int b = (int)(pix / ((long)W * H));
-    const T* o = om + pix * om_ldc;
+  const unsigned total = (unsigned)B * H * W * 9 * nq;
+  {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const unsigned q = i % (unsigned)nq;
+    const unsigned r = i / (unsigned)nq;
+    const int k = (int)(r % 9u);
+    const unsigned pix = r / 9u;
+    const int ox = (int)(pix % (unsigned)W);
+    const unsigned r2 = pix / (unsigned)W;
+    const int oy = (int)(r2 % (unsigned)H);
+    const unsigned b = r2 / (unsigned)H;
+    const T* o = om + (size_t)pix * om_ldc;
     const float dy = (float)o[2 * k], dx = (float)o[2 * k + 1];
     const float mask = 1.0f / (1.0f + expf(-(float)o[18 + k]));
     // torchvision: y = (oy * stride - pad) + i * dilation + offset_y (stride 1, pad 1)
@@ -98,13 +105,13 @@ __global__ __launch_bounds__(256) void dcn_sample(const T* __restrict__ x, int B
       const int y0 = (int)fy, x0 = (int)fx;
       const float ly = py - fy, lx = px - fx, hy = 1.f - ly, hx = 1.f - lx;
       const float wt[4] = {hy * hx, hy * lx, ly * hx, ly * lx};
-      const T* base = x + (long)b * H * W * C + q * V;
+      const T* base = x + (size_t)b * H * W * C + q * V;
 #pragma unroll
       for (int c4 = 0; c4 < 4; ++c4) {
         const int yy = y0 + (c4 >> 1), xx = x0 + (c4 & 1);
         if (yy >= 0 && yy <= H - 1 && xx >= 0 && xx <= W - 1) {
           Vec<T> t;
-          load_vec(base + ((long)yy * W + xx) * C, t);
+          load_vec(base + ((size_t)yy * W + xx) * C, t);
 #pragma unroll
           for (int e = 0; e < V; ++e) acc.v[e] += wt[c4] * t.v[e];
         }
@@ -112,7 +119,7 @@ __global__ __launch_bounds__(256) void dcn_sample(const T* __restrict__ x, int B
     }
 #pragma unroll
     for (int e = 0; e < V; ++e) acc.v[e] *= mask;
-    store_vec(cols + pix * (9L * C) + (long)k * C + q * V, acc);
+    store_vec(cols + (size_t)pix * (9 * C) + k * C + q * V, acc);
   }
 }
 
@@ -127,13 +134,16 @@ __global__ __launch_bounds__(256) void dwconvt_add(const T* __restrict__ src, in
   const int nq = C / V;
   const int p = f / 2, k = 2 * f;
   const int hu = (h - 1) * f - 2 * p + k, wu = (w - 1) * f - 2 * p + k;
-  const long total = (long)B * tH * tW * nq;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    const int q = (int)(i % nq);
-    const long pix = i / nq;
-    const int x = (int)(pix % tW);
-    const int y = (int)((pix / tW) % tH);
-    const int b = (int)(pix / ((long)tW * tH));
+  const unsigned total = (unsigned)B * tH * tW * nq;
+  {
+    const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const unsigned q = i % (unsigned)nq;
+    const unsigned pix = i / (unsigned)nq;
+    const int x = (int)(pix % (unsigned)tW);
+    const unsigned r = pix / (unsigned)tW;
+    const int y = (int)(r % (unsigned)tH);
+    const unsigned b = r / (unsigned)tH;
     Vec<T> acc;
 #pragma unroll
     for (int e = 0; e < V; ++e) acc.v[e] = 0.f;
@@ -153,25 +163,22 @@ __global__ __launch_bounds__(256) void dwconvt_add(const T* __restrict__ src, in
           const int ix = nx / f;
           if (ix >= w) continue;
           Vec<T> t;
-          load_vec(src + (((long)b * h + iy) * w + ix) * C + q * V, t);
-          const float* wp = weight + ((long)ky * k + kx) * C + q * V;
+          load_vec(src + (((size_t)b * h + iy) * w + ix) * C + q * V, t);
+          const float* wp = weight + (ky * k + kx) * C + q * V;
 #pragma unroll
           for (int e = 0; e < V; ++e) acc.v[e] += t.v[e] * wp[e];
         }
       }
     }
     Vec<T> s;
-    load_vec(add + pix * add_ldc + q * V, s);
+    load_vec(add + (size_t)pix * add_ldc + q * V, s);
 #pragma unroll
     for (int e = 0; e < V; ++e) acc.v[e] = acc.v[e] + s.v[e];
-    store_vec(out + pix * C + q * V, acc);
+    store_vec(out + (size_t)pix * C + q * V, acc);
   }
 }
 
-inline int grid_for(long threads) {
-  const long g = (threads + 255) / 256;
-  return (int)std::min<long>(std::max<long>(g, 1), 256L * 64);
-}
+inline int grid_for(long threads) { return (int)std::max<long>((threads + 255) / 256, 1); }
 
 }  // namespace dla
 
@@ -211,10 +218,12 @@ int dwconvt_t(const void* src, int B, int h, int w, int C, const float* weight, 
   return 0;
 }
 bool chunked(int C, int dtype) { return C > 0 && C % (16 / dtype_size(dtype)) == 0; }
+// one thread per 16-byte chunk, 32-bit thread indices
+bool fits(long B, long pix, long chunks) { return B * pix * chunks < (1L << 31); }
 }  // namespace
 
 int launch_maxpool2(const void* src, int B, int H, int W, int C, void* out, int Ho, int Wo, int dtype, hipStream_t s) {
-  if (!chunked(C, dtype) || Ho != (H + 1) / 2 || Wo != (W + 1) / 2) {
+  if (!chunked(C, dtype) || Ho != (H + 1) / 2 || Wo != (W + 1) / 2 || !fits(B, (long)Ho * Wo, C)) {
     set_error("maxpool2: channels must be whole 16-byte chunks and the output ceil(H/2) x ceil(W/2)");
     return 2;
   }
@@ -223,7 +232,7 @@ int launch_maxpool2(const void* src, int B, int H, int W, int C, void* out, int 
 
 int launch_dcn_sample(const void* x, int B, int H, int W, int C, const void* om, int om_ldc, void* cols, int dtype,
                       hipStream_t s) {
-  if (!chunked(C, dtype) || om_ldc < 27) {
+  if (!chunked(C, dtype) || om_ldc < 27 || !fits(B, (long)H * W, 9L * C)) {
     set_error("dcn_sample: channels must be whole 16-byte chunks, offset/mask tensor >= 27 channels");
     return 2;
   }
@@ -232,7 +241,7 @@ int launch_dcn_sample(const void* x, int B, int H, int W, int C, const void* om,
 
 int launch_dwconvt_add(const void* src, int B, int h, int w, int C, const float* weight, int f, const void* add,
                        int add_ldc, void* out, int tH, int tW, int sy, int sx, int dtype, hipStream_t s) {
-  if (!chunked(C, dtype) || f < 1 || add_ldc < C || sy < 0 || sx < 0) {
+  if (!chunked(C, dtype) || f < 1 || add_ldc < C || sy < 0 || sx < 0 || !fits(B, (long)tH * tW, C)) {
     set_error("dwconvt_add: bad geometry");
     return 2;
   }

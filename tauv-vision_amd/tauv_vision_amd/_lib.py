@@ -53,6 +53,9 @@ EXPORTS = {
     "tv_decode": ([c_vp, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_i64), c_vp, ctypes.POINTER(c_i64), c_vp,
                    ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_vp,
                    ctypes.POINTER(c_i64), c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
+    "tv_yolact_box_decode": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp], c_i32),
+    "tv_yolact_fast_nms": ([c_vp, c_i32, c_i32, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp, c_vp], c_i32),
+    "tv_yolact_assemble_mask": ([c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
     "tv_last_error": ([], ctypes.c_char_p),
     "tv_version": ([], ctypes.c_char_p),
 }

@@ -7,22 +7,38 @@ preprocess (fused) -> Centernet forward -> decode (sigmoid + 3x3 peak NMS + exac
 
 "R18" = reference Centernet(DLABackbone([2]*5, [128]*6, downsamples=2)) with 4 plain classes
 (heads [4, 2, 2]): SURVEY.md §0 maps BASELINE's "CenterNet-R18" to this model.
-Weights: seeded synthetic (xavier convs, randomised BN; no checkpoints travel).
+Weights: seeded synthetic (xavier convs, randomised BN; no checkpoints travel) — the same
+recipe as the committed golden fixture tests/golden/model_r18_c128_b1_480x640.npz, so the
+parity leg compares the benchmarked kernels against the reference's own outputs.
+
+Extra keys next to the contract's (all measured in this run, on rank 0):
+  roofline         dominant conv kernel: per-launch HIP events on the launch stream
+  decode_roofline  the decode kernels' achieved HBM GB/s (algorithmic bytes / event time)
+  parity           the timed precision's detections on the golden frame (inside a B-frame
+                   batch) vs the reference's decode(K=100) records (tests/golden/detcmp.py)
+  fp32_value       frames/s of the same step in fp32 (the reference's arithmetic)
+  latency_b1       B=1 hipGraph replay (forward + decode + D2H), in fp16 and in bf16
+  host_feed        frames/s when the u8 frames start in pinned host memory (H2D on a
+                   side stream, double-buffered, overlapped with the previous step)
+  cpu_baseline     the oracle's PyTorch-CPU forward + decode on this host
 
 Launch:  python bench.py [--gpus 1] [--steps 20] [--warmup 5]
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-Rank 0 prints one JSON line.
+Rank 0 prints one JSON line. Any TV_* environment knob (kernel-choice overrides, an
+alternative library) makes the bench refuse to run unless --allow-env-knobs is given, and
+is then stamped into the line as "env_knobs".
 """
 import argparse
-import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tauv-vision_amd"))
 
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
@@ -33,7 +49,9 @@ from tauv_vision_amd.weights import seeded_state_dict  # noqa: E402
 
 HEIGHTS, CHANNELS, DOWNSAMPLES, N_LABELS = [2] * 5, [128] * 6, 2, 4
 PEAK_TFLOPS = {"fp16": 2500.0, "bf16": 2500.0, "fp32": 157.3}  # dense MFMA, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
 METRIC = "frames/sec CenterNet-R18 640x480 batch=1 & 64; 1/2/4/8 MI355X + %roofline"
+GOLDEN = {"r18": ("model_r18_c128_b1_480x640", 105), "dla34": ("dla34_b1_480x640_kp", 202)}
 
 
 def build_model(precision, device, arch="r18"):
@@ -65,15 +83,40 @@ class Pipeline:
         self.host = torch.empty((B, K, 10), dtype=torch.float32, pin_memory=True)
         self.host_counts = torch.empty((B,), dtype=torch.int32, pin_memory=True)
 
+    def decode(self):
+        p = self.pred
+        return self.dec(p.heatmap, p.size, p.offset, p.depth, 0, self.mc.downsample_ratio, self.mc.in_h,
+                        self.mc.in_w, self.thr)
+
     def step(self, frames, gather=None):
         self.eng.forward_u8(frames, self.out)
-        p = self.pred
-        rec, cnt = self.dec(p.heatmap, p.size, p.offset, p.depth, 0, self.mc.downsample_ratio, self.mc.in_h,
-                            self.mc.in_w, self.thr)
+        rec, cnt = self.decode()
         if gather is not None:
             gather(rec, cnt)
         self.host.copy_(rec, non_blocking=True)
         self.host_counts.copy_(cnt, non_blocking=True)
+
+
+def timed(fn, steps, warmup, world=1, device=None):
+    """W untimed calls, then K timed ones bracketed by barrier + synchronize; max over ranks."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def load_traffic(kernel, batch, precision):
@@ -110,8 +153,8 @@ def conv_roofline(pipe, frames, precision, reps=3):
         else:
             for b, o in zip(best, ops):
                 b[1] = min(b[1], o[1])
-    if os.environ.get("TV_PROFILE_OUT"):
-        with open(os.environ["TV_PROFILE_OUT"], "w") as f:
+    if os.environ.get("BENCH_PROFILE_OUT"):
+        with open(os.environ["BENCH_PROFILE_OUT"], "w") as f:
             json.dump([{"op": o[0], "ms": o[1], "gflop": o[2] / 1e9, "kernel": o[3]} for o in best], f, indent=0)
     conv = [o for o in best if o[2] > 0]
     kern = {}
@@ -136,6 +179,156 @@ def conv_roofline(pipe, frames, precision, reps=3):
                            for k, v in kern.items()},
             "top_launches": [{"op": o[0], "ms": round(o[1], 4),
                               "tflops": round(o[2] / max(o[1], 1e-9) / 1e9, 1)} for o in top]}
+
+
+def decode_roofline(pipe, reps=20):
+    """HIP-event time of the device decode (on the stream it launches on) over the bench
+    batch's head tensor. Algorithmic bytes: the heatmap read once
+    (B*C*Ho*Wo*4 B) + per record the size/offset gathers (4 x 4 B) + the record written
+    (10 x 4 B) + counts."""
+    B, C, H, W, K = pipe.dec.shape
+    s = torch.cuda.current_stream()
+    pipe.decode()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    best = None
+    for _ in range(reps):
+        ev[0].record(s)
+        pipe.decode()
+        ev[1].record(s)
+        ev[1].synchronize()
+        t = ev[0].elapsed_time(ev[1])
+        best = t if best is None else min(best, t)
+    nbytes = B * C * H * W * 4 + B * K * (16 + 40) + B * 4
+    gbs = nbytes / (best * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4), "ms": round(best, 4), "bytes": nbytes,
+            "batch": B, "K": K}
+
+
+def parity_leg(model, oc, mc, arch, B, K, device):
+    """The timed precision's engine + decode on the golden frame (placed at frames 0 and B//2+8,
+    one per concurrent slice, among random frames) vs the reference's decode(K=100) records
+    and Prediction.heatmap stored in tests/golden (data, not oracle code)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from detcmp import peak_parity
+    name, seed = GOLDEN[arch]
+    g = np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"))
+    gen = torch.Generator().manual_seed(seed)
+    frame = torch.randint(0, 256, (1, mc.in_h, mc.in_w, 3), generator=gen, dtype=torch.uint8)
+    frames = torch.randint(0, 256, (B, mc.in_h, mc.in_w, 3), generator=torch.Generator().manual_seed(7),
+                           dtype=torch.uint8)
+    slots = sorted({0, min(B - 1, B // 2 + 8)})
+    for sl in slots:
+        frames[sl] = frame[0]
+    pipe = Pipeline(model, oc, mc, B, K, 0.0, device)
+    pipe.step(frames.to(device))
+    torch.cuda.synchronize()
+    rec = pipe.host.numpy()
+    res = {"agreement": 1.0, "determined": 0, "determined_found": 0, "extra_ok": True, "max_score_err": 0.0,
+           "max_box_err": 0.0, "heatmap_drift": 0.0}
+    for sl in slots:
+        hm = pipe.pred.heatmap[sl].cpu().numpy()
+        drift = float(np.abs(hm - g["heatmap"][0]).max())
+        pp = peak_parity(rec[sl:sl + 1], g["heatmap"][:1], g["decode_k100_index"][:1], g["decode_k100"][:1],
+                         max(drift, 1e-6))
+        res["agreement"] = min(res["agreement"], pp["agreement"])
+        res["determined"] += pp["determined"]
+        res["determined_found"] += pp["determined_found"]
+        res["extra_ok"] &= pp["extra_ok"]
+        for k in ("max_score_err", "max_box_err"):
+            res[k] = max(res[k], pp[k])
+        res["heatmap_drift"] = max(res["heatmap_drift"], drift)
+    res = {k: (round(v, 7) if isinstance(v, float) else v) for k, v in res.items()}
+    res.update({"K": K, "frames_checked": len(slots), "batch": B,
+                "reference": f"tests/golden/{name}.npz (reference decode K=100 records)"})
+    return res
+
+
+def latency_b1(model, oc, mc, K, thr, device, frames, steps):
+    p1 = Pipeline(model, oc, mc, 1, K, thr, device)
+    f1 = frames[:1].contiguous()
+    s = torch.cuda.Stream(device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            p1.step(f1)
+    torch.cuda.current_stream(device).wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        p1.step(f1)
+    for _ in range(10):
+        graph.replay()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    lat = (time.perf_counter() - t1) / steps
+    return {"batch": 1, "ms_per_frame": round(lat * 1e3, 4), "frames_per_sec": round(1.0 / lat, 2),
+            "path": "hipGraph replay of forward_u8 + decode + D2H", "n_gpus_used": 1}
+
+
+def host_feed(pipe, frames, steps, warmup, device):
+    """Frames start in pinned host memory: step i's H2D copy (side stream, double buffer)
+    overlaps step i-1's compute; the compute stream waits for its copy's event."""
+    B = pipe.B
+    host = [frames.cpu().pin_memory(), frames.cpu().pin_memory()]
+    dev = [torch.empty_like(frames), torch.empty_like(frames)]
+    copy_s = torch.cuda.Stream(device)
+    comp = torch.cuda.current_stream(device)
+    done = [torch.cuda.Event(), torch.cuda.Event()]
+    used = [torch.cuda.Event(), torch.cuda.Event()]
+    for e in used:
+        e.record(comp)
+    state = {"i": 0}
+
+    def issue(i):
+        j = i & 1
+        with torch.cuda.stream(copy_s):
+            copy_s.wait_event(used[j])
+            dev[j].copy_(host[j], non_blocking=True)
+            done[j].record(copy_s)
+
+    def step():
+        i = state["i"]
+        if i == 0:
+            issue(0)
+        issue(i + 1)  # next step's frames in flight during this step
+        comp.wait_event(done[i & 1])
+        pipe.step(dev[i & 1])
+        used[i & 1].record(comp)
+        state["i"] = i + 1
+
+    el = timed(step, steps, warmup)
+    nbytes = B * frames[0].numel()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(copy_s)
+    with torch.cuda.stream(copy_s):
+        dev[0].copy_(host[0], non_blocking=True)
+    ev[1].record(copy_s)
+    ev[1].synchronize()
+    h2d = nbytes / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9
+    return {"value": round(B * steps / el, 2), "unit": "frames/sec", "batch": B,
+            "h2d_GBps": round(h2d, 1), "bytes_per_step": nbytes,
+            "path": "pinned host u8 frames -> H2D on a side stream (double-buffered) -> forward_u8 + decode + D2H"}
+
+
+def fp32_throughput(arch, mc, B, K, thr, device, frames, steps):
+    model, oc, _ = build_model("fp32", device, arch)
+    pipe = Pipeline(model, oc, mc, B, K, thr, device)
+    el = timed(lambda: pipe.step(frames), steps, 1)
+    return round(B * steps / el, 2)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(sd, seconds, K, thr, arch="r18"):
@@ -165,8 +358,13 @@ def cpu_baseline(sd, seconds, K, thr, arch="r18"):
             if el >= seconds:
                 break
     return {"value": round(n / el, 4), "unit": "frames/sec", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{n} single frames 640x480 (B=1), fp32 forward + decode(K={K}) in {el:.1f}s; "
                       f"oracle/ PyTorch-CPU restatement, bit-identical to the reference on CPU"}
+
+
+def env_knobs():
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("TV_")}
 
 
 def main():
@@ -181,10 +379,16 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-b1", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip parity / fp32 / host-feed / decode legs")
     ap.add_argument("--b1-steps", type=int, default=200)
+    ap.add_argument("--fp32-steps", type=int, default=3)
+    ap.add_argument("--allow-env-knobs", action="store_true")
     ap.add_argument("--model", default="r18", choices=["r18", "dla34"],
                     help="r18: the BASELINE CenterNet-R18 (headline); dla34: CenterpointDLA34, heads [4,4,8,2,2]")
     args = ap.parse_args()
+    knobs = env_knobs()
+    if knobs and not args.allow_env_knobs:
+        sys.exit(f"bench.py: TV_* environment knobs set ({knobs}); unset them or pass --allow-env-knobs")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -203,54 +407,31 @@ def main():
 
     # detections of every rank on every rank: one RCCL all-gather of the packed records
     gather = RecordGather(B, K, device) if world > 1 else None
-
-    for _ in range(args.warmup):
-        pipe.step(frames, gather)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        pipe.step(frames, gather)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(lambda: pipe.step(frames, gather), args.steps, args.warmup, world, device)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
     # roofline of the dominant kernel (separate pass with per-launch events)
     roof = conv_roofline(pipe, frames, args.precision)
     flops_frame = pipe.eng.geom["flops_per_frame"]
+    extras = {}
+    if rank == 0 and not args.no_extras:
+        extras["decode_roofline"] = decode_roofline(pipe)
+        if args.precision != "fp32":
+            extras["parity"] = parity_leg(model, oc, mc, args.model, B, K, device)
+        extras["host_feed"] = host_feed(pipe, frames, max(5, args.steps // 2), 2, device)
 
     b1 = None
     if not args.no_b1:
-        p1 = Pipeline(model, oc, mc, 1, K, args.thr, device)
-        f1 = frames[:1].contiguous()
-        s = torch.cuda.Stream(device)
-        s.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(s):
-            for _ in range(3):
-                p1.step(f1)
-        torch.cuda.current_stream(device).wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=s):
-            p1.step(f1)
-        for _ in range(10):
-            graph.replay()
+        b1 = {args.precision: latency_b1(model, oc, mc, K, args.thr, device, frames, args.b1_steps)}
+        if args.precision == "fp16":  # BASELINE config 2 names bf16 for the latency path
+            m16, oc16, _ = build_model("bf16", device, args.model)
+            b1["bf16"] = latency_b1(m16, oc16, mc, K, args.thr, device, frames, args.b1_steps)
+            del m16
+    if rank == 0 and not args.no_extras and args.precision != "fp32":
+        del pipe
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.b1_steps):
-            graph.replay()
-        torch.cuda.synchronize()
-        lat = (time.perf_counter() - t1) / args.b1_steps
-        b1 = {"batch": 1, "ms_per_frame": round(lat * 1e3, 4), "frames_per_sec": round(1.0 / lat, 2),
-              "path": "hipGraph replay of forward_u8 + decode + D2H", "n_gpus_used": 1}
+        extras["fp32_value"] = fp32_throughput(args.model, mc, B, K, args.thr, device, frames, args.fp32_steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -260,7 +441,8 @@ def main():
         workload = (f"CenterNet-R18 (Centernet+DLABackbone [2]*5/[128]*6, ds 2, heads [4,2,2]) " if args.model == "r18"
                     else "CenterpointDLA34 (DLA-34 + DLAUp/IDAUp with DCNv2, heads [4,4,8,2,2]) ")
         line = {
-            "metric": METRIC if args.model == "r18" else METRIC.replace("CenterNet-R18", "CenterpointDLA34"), "value": round(value, 2), "unit": "frames/sec", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC if args.model == "r18" else METRIC.replace("CenterNet-R18", "CenterpointDLA34"),
+            "value": round(value, 2), "unit": "frames/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"workload": workload + f"640x480 u8 frames, batch={B}/GPU, forward + decode(K={K}, thr={args.thr})",
@@ -270,6 +452,9 @@ def main():
             "e2e_frac_of_peak": round(value * flops_frame / 1e12 / PEAK_TFLOPS[args.precision], 4),
             "roofline": roof, "latency_b1": b1, "cpu_baseline": cpu,
         }
+        line.update(extras)
+        if knobs:
+            line["env_knobs"] = knobs
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

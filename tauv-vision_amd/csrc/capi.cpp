@@ -213,9 +213,7 @@ int tv_yolact_assemble_mask(const float* proto, int32_t K, int32_t H, int32_t W,
 
 int tv_decode_workspace_size(int32_t B, int32_t C, int32_t H, int32_t W, int32_t K, int64_t* bytes) {
   if (!bytes || B < 1 || C < 1 || H < 1 || W < 1 || K < 1) { set_error("bad argument"); return TV_EINVAL; }
-  int64_t peaks = ((int64_t)B * C * H * W * 4 + 255) / 256 * 256;
-  int64_t sel = ((int64_t)B * K * 8 + 255) / 256 * 256;
-  *bytes = peaks + sel;
+  *bytes = (int64_t)select_workspace_bytes(B, C, H, W, K);
   return TV_OK;
 }
 
@@ -234,21 +232,16 @@ int tv_decode(const float* heat, const int64_t hs[4], const float* size, const i
     if (mode == 0 && (!offset || !os)) { set_error("decode needs the offset head"); return TV_EINVAL; }
     if (depth && !ds) { set_error("depth strides missing"); return TV_EINVAL; }
     hipStream_t s = (hipStream_t)stream;
-    float* peaks = (float*)ws;
-    int64_t poff = ((int64_t)B * C * H * W * 4 + 255) / 256 * 256;
-    float* score = (float*)((char*)ws + poff);
-    int32_t* index = (int32_t*)((char*)ws + poff + (int64_t)B * K * 4);
-    rc = launch_peaks(heat, hs, B, C, H, W, 3, 1, peaks, s);
-    if (rc) return rc;
-    rc = launch_topk(peaks, B, (int64_t)C * H * W, K, score, index, s);
-    if (rc) return rc;
     DecodeParams p{};
-    p.score = score;
-    p.index = index;
     p.B = B; p.K = K; p.C = C; p.H = H; p.W = W;
-    p.size = size; p.size_st = ss;
-    p.offset = offset; p.offset_st = os;
-    p.depth = depth; p.depth_st = ds;
+    p.size = size;
+    p.offset = offset;
+    p.depth = depth;
+    for (int i = 0; i < 4; ++i) {
+      p.size_st[i] = ss[i];
+      p.offset_st[i] = offset ? os[i] : 0;
+      p.depth_st[i] = depth ? ds[i] : 0;
+    }
     p.depth_mode = mode == 0 ? 0 : 1;
     p.pos_mode = mode == 0 ? 0 : 1;
     p.ratio = ratio; p.in_h = in_h; p.in_w = in_w;
@@ -262,7 +255,7 @@ int tv_decode(const float* heat, const int64_t hs[4], const float* size, const i
     }
     p.records = records;
     p.counts = counts;
-    return launch_decode_records(p, s);
+    return launch_select(heat, hs, B, C, H, W, 1, 1, K, ws, (size_t)ws_bytes, nullptr, nullptr, &p, s);
   })
 }
 

@@ -76,24 +76,12 @@ struct ConvParams {
   const float* head_b;  // [ntiles][32] 1x1 bias on the first tile of each head, zeros elsewhere
   int head_ldc;
   int head_row0[8], head_nrows[8];
-  int ablate;           // timing experiments only (env TV_ABLATE): 1 no main-loop DMA, 2 no MFMA
-  unsigned long long* stamps;  // diagnostics only (env TV_STAMPS): per block kStampWords words
 };
-// per-block stamp record: s_memtime at entry, first stage landed, main loop done, end;
-// s_memrealtime at entry and end; HW_ID; XCC_ID
-// (+ persistent kernels: [8] cycles stalled in waits/barriers, [9] epilogue cycles, [10] tiles)
-constexpr int kStampWords = 12;
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
 int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
                      hipStream_t s);
 constexpr int kPipeTileM = 256;
-
-// Halo-tile 3x3 / stride 1 / pad 1 variant (conv_halo.hip): 256-pixel blocks of tw columns
-// (tw = 16 or 32); ConvParams.mtiles must be halo_tiles(B, H, W, tw).
-int launch_conv_halo(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int tw,
-                     hipStream_t s);
-int halo_tiles(int B, int H, int W, int tw);
 
 // Persistent halo-tile 3x3 / stride 1 / pad 1 kernel (conv3x3.hip), fp16/bf16: 512-pixel
 // tiles of tw (16 or 32) columns; ConvParams.mtiles = conv3x3_tiles(B, H, W, tw); `grid`
@@ -130,7 +118,6 @@ struct StemParams {
   int out_ldc, N;
   const void* weight; // stem_weight_bytes() in B-fragment order (stem_fragment_order)
   const float* bias;  // [>= N] fp32, BN folded
-  int ablate;         // timing experiments only (env TV_STEM_ABLATE): 1 no stores, 2 no MFMA, 4 no staging
 };
 size_t stem_weight_bytes();
 void stem_fragment_order(const uint16_t* w, int Npad, int Kpad, uint16_t* out);
@@ -149,7 +136,6 @@ struct ConvTParams {
   int out_ldc;
   int B, s, tH, tW, sy, sx;
   int tpw, nchunks, np;  // schedule (convt_schedule): tiles per wave, workgroups per phase group, phases per group
-  int ablate;         // timing experiments only (env TV_CONVT_ABLATE): 1 no stores, 2 no MFMA, 4 no skip loads
 };
 bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc);
 void convt_schedule(ConvTParams& p, int cu_count);
@@ -188,13 +174,12 @@ int launch_peaks(const float* heat, const int64_t st[4], int B, int C, int H, in
                  int apply_sigmoid, float* peaks, hipStream_t s);
 int launch_topk(const float* peaks, int B, int64_t n, int K, float* score, int32_t* index,
                 hipStream_t s);
+// Detection-record gather of the final decode stage (passed by value to the kernel).
 struct DecodeParams {
-  const float* score;  // [B][K]
-  const int32_t* index;
   int B, K, C, H, W;
-  const float* size;    const int64_t* size_st;    // element (b,y,x,ch) strides
-  const float* offset;  const int64_t* offset_st;  // may be null (keypoint object path)
-  const float* depth;   const int64_t* depth_st;   // may be null
+  const float* size;    int64_t size_st[4];    // element (b,y,x,ch) strides
+  const float* offset;  int64_t offset_st[4];  // may be null (keypoint object path)
+  const float* depth;   int64_t depth_st[4];   // may be null
   int depth_mode;       // 0: 1/sigmoid(d) - 1 (decode), 1: 1/sigmoid(d) (decode_keypoints)
   int ratio, in_h, in_w, out_h, out_w;
   int pos_mode;         // 0: (R*i + offset)/in (decode), 1: i/out (decode_keypoints)
@@ -204,7 +189,13 @@ struct DecodeParams {
   float* records;       // [B][K][10]: label, score, y, x, h, w, depth, flat index, aux0, aux1
   int32_t* counts;      // [B]
 };
-int launch_decode_records(const DecodeParams& p, hipStream_t s);
+// Exact per-image top-K of the (sigmoid ->) 3x3-NMS keys of a strided [B,C,H,W] fp32 view (nms 0:
+// plain top-K), ties to the smaller flat index: tile_select + merge_select (decode.hip). Writes
+// score / flat index [B][K] (either may be null) and, when rec != null, the detection records.
+size_t select_workspace_bytes(int B, int C, int H, int W, int K);
+int launch_select(const float* heat, const int64_t st[4], int B, int C, int H, int W, int nms, int apply_sigmoid,
+                  int K, void* ws, size_t ws_bytes, float* score, int32_t* index, const DecodeParams* rec,
+                  hipStream_t s);
 // heatmap_detect()'s (index[B,K,2], label[B,K]) as int64 from flat top-K indices.
 int launch_index_split(const int32_t* flat, int B, int K, int H, int W, int64_t* index, int64_t* label,
                        hipStream_t s);

@@ -176,11 +176,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     stride = G;
   }
   const int ntl = first < end ? (end - first + stride - 1) / stride : 0;
-  unsigned long long st0 = 0, rt0 = 0, st1 = 0, stall = 0, epi = 0;
-  if (p.stamps) {
-    st0 = __builtin_amdgcn_s_memtime();
-    rt0 = __builtin_amdgcn_s_memrealtime();
-  }
   if (ntl == 0) return;
   const int S_tot = ntl * SPTK;
 
@@ -491,7 +486,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
     read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   }
-  if (p.stamps) st1 = __builtin_amdgcn_s_memtime();
 
   int s = 0;   // global k-step
   int tl = 0;  // tile index within this block's list
@@ -517,15 +511,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     //    tap 4): younger = weight loads of taps 4, 5, 6, 7 + the tap-5 halo piece.
     static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
     auto wl = [&](int q) { return q >= 0 ? 1 : 0; };
-    unsigned long long tw0 = 0;
-    if (p.stamps) tw0 = __builtin_amdgcn_s_memtime();
     if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
     if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (p.stamps) stall += __builtin_amdgcn_s_memtime() - tw0;
 
     constexpr int NTAP = TAP == 8 ? (RES ? 9 : 0) : TAP == 9 ? 0 : TAP + 1;
     const bool do_r = s + 1 < S_tot;
@@ -624,20 +615,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     cblock(IC<1>{});
     cblock(IC<2>{});
     cblock(IC<3>{});
-    unsigned long long te0 = 0;
-    if (p.stamps) te0 = __builtin_amdgcn_s_memtime();
     epilogue(cur_fr, cur_y0, cur_x0, cur_nt);
-    if (p.stamps) epi += __builtin_amdgcn_s_memtime() - te0;
     ++tl;
     if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
-  }
-  if (p.stamps && tid == 0) {
-    unsigned long long* w = p.stamps + (size_t)blockIdx.x * kStampWords;
-    write_stamps(w, st0, st1, st1, rt0);
-    w[8] = stall;
-    w[9] = epi;
-    w[10] = (unsigned long long)ntl;
-    w[11] = (unsigned long long)S_tot;
   }
 }
 

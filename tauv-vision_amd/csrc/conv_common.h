@@ -74,20 +74,4 @@ __device__ __forceinline__ void store_chunk(OutT* dst, const float* v) {
   gstore16(dst, make_uint4(w[0], w[1], w[2], w[3]));
 }
 
-// diagnostics (ConvParams.stamps): one record per block, written by thread 0
-__device__ __forceinline__ void write_stamps(unsigned long long* w, unsigned long long st0, unsigned long long st1,
-                                             unsigned long long st2, unsigned long long rt0) {
-  w[0] = st0;
-  w[1] = st1;
-  w[2] = st2;
-  w[3] = __builtin_amdgcn_s_memtime();
-  w[4] = rt0;
-  w[5] = __builtin_amdgcn_s_memrealtime();
-  unsigned hw, xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  w[6] = hw;
-  w[7] = xcc;
-}
-
 }  // namespace tv

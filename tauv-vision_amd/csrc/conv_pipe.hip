@@ -61,11 +61,6 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  unsigned long long st0 = 0, st1 = 0, st2 = 0, rt0 = 0;
-  if (p.stamps) {
-    st0 = __builtin_amdgcn_s_memtime();
-    rt0 = __builtin_amdgcn_s_memrealtime();
-  }
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): LDS-DMA base in M0
 
   const int nb = p.mtiles * p.ntiles;
@@ -208,7 +203,6 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     }
   };
   auto mfmas = [&](const u32x4(&f)[4][4]) __attribute__((always_inline)) {
-    if (p.ablate & 2) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -223,7 +217,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave: stage ks+1 visible, slot ks%S released
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + S < total_ks && !(p.ablate & 1)) issue(ks + S, ks % S);
+    if (ks + S < total_ks) issue(ks + S, ks % S);
     if (ks + 1 < total_ks) read_frags(ks + 1, nxt);
     __builtin_amdgcn_sched_barrier(0);
     mfmas(cur);
@@ -237,7 +231,6 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
-  if (p.stamps) st1 = __builtin_amdgcn_s_memtime();
   read_frags(0, fa);
   for (int ks = 0; ks < total_ks; ks += 2) {
     step(ks, fa, fb);
@@ -246,7 +239,6 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
 
   // ---- epilogue: bias + activation into an fp32 staging tile, then 16-byte stores
   __syncthreads();
-  if (p.stamps) st2 = __builtin_amdgcn_s_memtime();
   float* stg = reinterpret_cast<float*>(smem);
   constexpr int SR = EROW / 4;
 #pragma unroll
@@ -331,11 +323,6 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
       }
       store_chunk<OutT>(reinterpret_cast<OutT*>(out_ptr) + toff[k] * p.out_ldc + co, v);
     }
-  }
-  if (p.stamps) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) write_stamps(p.stamps + (size_t)blockIdx.x * kStampWords, st0, st1, st2, rt0);
   }
 }
 

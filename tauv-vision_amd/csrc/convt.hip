@@ -112,7 +112,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     for (int j = 0; j < KJ; ++j) S.x[j] = gload16(src + 16 * j);
   };
   auto load_a = [&](int t, int ph, ASet& S) __attribute__((always_inline)) {
-    if (p.ablate & 4) return;
     const long long tg = target(t, ph);
     const T* add = reinterpret_cast<const T*>(p.add) + (tg < 0 ? 0 : tg) * p.add_ldc + 8 * lh;
 #pragma unroll
@@ -131,7 +130,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       uint4 wv[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) wv[i] = *reinterpret_cast<const uint4*>(wl + i * 32 * WPITCH + j * 32);
-      if (!(p.ablate & 2)) {
+      {
 #pragma unroll
         for (int i = 0; i < 4; ++i) Mfma<T>::run(wv[i], X.x[j], acc[i]);
       }
@@ -165,7 +164,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = pack2<T>(lo_f<T>(sw[e]) + f[2 * e], hi_f<T>(sw[e]) + f[2 * e + 1]);
-        if (tg >= 0 && !(p.ablate & 1)) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
+        if (tg >= 0) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
       }
   };
 

@@ -1,22 +1,33 @@
-// Heatmap peak decode on gfx950: sigmoid + k x k peak NMS, exact per-image top-K, and the
-// per-detection gather of size/offset/depth (decode.py:179-279, 51-98).
+// Heatmap peak decode on gfx950: sigmoid + 3x3 peak NMS, exact per-image top-K and the
+// per-detection gather of size/offset/depth (decode.py:179-279, 51-98), as two launches that
+// read the head tensor once:
 //
-//  peaks   : one thread per heatmap element, any input strides (NCHW views or the
-//            engine's NHWC head tensor); output is the dense heatmap_nms() map.
-//  topk    : one 1024-thread workgroup per image. Exact radix select on the 64-bit key
-//            (orderable score bits << 32 | ~flat_index), so the result is the true top-K
-//            with ties broken toward the smaller flat index (torch.topk leaves tie order
-//            unspecified, decode.py:269). 11-bit digit histograms in LDS; once the
-//            threshold bucket holds <= 4096 keys they are sorted in LDS (bitonic).
-//  records : one workgroup per image; [label, score, y, x, h, w, depth, flat index, aux0,
-//            aux1] per detection (aux = the keypoint affinity pair of decode.py:121-122)
-//            plus the count of scores >= threshold (the host loop's break, decode.py:207).
+//  tile_select : grid B x tiles. A tile is (channel group, row band, column band) of one
+//                image. Its elements plus a one-pixel halo are loaded ONCE into LDS (sigmoid
+//                applied once per element, out-of-image = -inf like max_pool2d's implicit
+//                padding), each thread forms the 3x3 NMS keys of its 16 elements in
+//                registers, and an exact block radix select (8-bit digits over the 64-bit key
+//                = orderable score bits << 32 | ~flat index) keeps the tile's top K, written
+//                unordered to a fixed K-slot list (zero-key padded when the tile has < K).
+//  merge       : grid B (x groups). Up to kMergeCap candidate keys per workgroup in registers,
+//                the same radix select -> top K; the final level sorts them (bitonic, LDS)
+//                and writes score / flat index and, for tv_decode, the detection records
+//                ([label, score, y, x, h, w, depth, flat index, aux0, aux1] + the count of
+//                scores >= threshold, the host loop's break at decode.py:207).
+// Keys are unique (the flat index is in the low word), so the selection is exact and ties
+// in score resolve toward the smaller flat index (torch.topk: unspecified, decode.py:269).
+//
+//  peaks       : heatmap_nms() as a dense map (tv_heatmap_nms, parity API only).
 #include "common.h"
+
+#include <algorithm>
+#include <vector>
 
 namespace tv {
 
 __device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// ---- heatmap_nms as a dense map (tv_heatmap_nms) ----------------------------------------
 __global__ void peaks_kernel(const float* __restrict__ heat, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
                              int B, int C, int H, int W, int r, int apply_sigmoid, float* __restrict__ out) {
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -55,10 +66,13 @@ int launch_peaks(const float* heat, const int64_t st[4], int B, int C, int H, in
   return 0;
 }
 
-// ---- exact top-K --------------------------------------------------------------------
-constexpr int kSelThreads = 1024;
-constexpr int kBins = 2048;
-constexpr int kCap = 4096;
+// ---- keys and the block radix select ----------------------------------------------------
+constexpr int kTileThreads = 512;
+constexpr int kTilePer = 16;                             // keys per thread in tile_select
+constexpr int kTileElems = kTileThreads * kTilePer;      // 8192 elements per tile
+constexpr int kMergeThreads = 1024;
+constexpr int kMergePer = 16;
+constexpr int kMergeCap = kMergeThreads * kMergePer;     // 16384 candidates per merge workgroup
 constexpr int kMaxK = 1024;
 
 __device__ __forceinline__ uint32_t order_bits(float f) {
@@ -68,43 +82,244 @@ __device__ __forceinline__ uint32_t order_bits(float f) {
 __device__ __forceinline__ float unorder_bits(uint32_t u) {
   return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
 }
+// > 0 for every real element (flat index < 2^32 - 1), so 0 marks padding
 __device__ __forceinline__ uint64_t make_key(float f, uint32_t idx) {
   return ((uint64_t)order_bits(f) << 32) | (uint64_t)(0xFFFFFFFFu - idx);
 }
 
-// block-wide inclusive scan of one int per thread (1024 threads = 16 waves)
-__device__ int block_scan_incl(int v, int* wsum) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int t = __shfl_up(v, o);
-    if (lane >= o) v += t;
-  }
-  if (lane == 63) wsum[wave] = v;
-  __syncthreads();
-  if (wave == 0) {
-    int w = lane < 16 ? wsum[lane] : 0;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      int t = __shfl_up(w, o);
-      if (lane >= o) w += t;
-    }
-    if (lane < 16) wsum[lane] = w;
-  }
-  __syncthreads();
-  int r = v + (wave > 0 ? wsum[wave - 1] : 0);
-  __syncthreads();
-  return r;
+struct SelectShared {
+  int hist[256];
+  unsigned long long red_lo[16], red_hi[16];
+  int red_n[16];
+  int sel_digit, sel_above, sel_count, nreal, nout;
+};
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m), hi = __shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
 }
 
+// block-wide (min, max) of 64-bit values and sum of ints
+template <int NT>
+__device__ void block_minmax_sum(uint64_t& lo, uint64_t& hi, int& n, SelectShared& sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t l = shfl_xor_u64(lo, m), h = shfl_xor_u64(hi, m);
+    lo = l < lo ? l : lo;
+    hi = h > hi ? h : hi;
+    n += __shfl_xor(n, m);
+  }
+  if (lane == 0) { sh.red_lo[wave] = lo; sh.red_hi[wave] = hi; sh.red_n[wave] = n; }
+  __syncthreads();
+  lo = ~0ull; hi = 0; n = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    lo = sh.red_lo[w] < lo ? sh.red_lo[w] : lo;
+    hi = sh.red_hi[w] > hi ? sh.red_hi[w] : hi;
+    n += sh.red_n[w];
+  }
+  __syncthreads();
+}
+
+// Threshold T with |{real keys >= T}| == need (1 <= need <= number of real keys; real keys are
+// non-zero). Keys are unique. Every pass first narrows the key range to the keys still in play
+// (block min / max), then histograms the 8-bit digit just below their common high bits — so
+// passes never spend themselves on bits all candidates share, and LDS atomics spread over the
+// candidates' actual value range (a flat heatmap puts every score in one fixed-digit bucket).
+// Keys of positive scores and the rest (NMS-suppressed zeros, negatives) are split first: when
+// fewer than `need` keys have a positive score, all of them are in and the rest is selected
+// among the others (ties at score 0 go to the smaller flat index).
+template <int NT, int PER>
+__device__ uint64_t block_select(const uint64_t (&k)[PER], int need, SelectShared& sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr uint64_t kZ = (0x80000000ull << 32) | 0xFFFFFFFFull;  // largest key of score +0.0
+  int upper = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) upper += k[j] > kZ;
+  {
+    uint64_t a = ~0ull, b = 0;
+    block_minmax_sum<NT>(a, b, upper, sh);
+  }
+  const bool lower_mode = upper < need;
+  if (lower_mode) need -= upper;
+  uint64_t prefix = 0, pmask = 0;
+  for (;;) {
+    // keys still in play: eligible class, matching the fixed high bits
+    uint64_t lo = ~0ull, hi = 0;
+    int dummy = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint64_t key = k[j];
+      const bool el = key != 0 && (key > kZ) != lower_mode && (key & pmask) == prefix;
+      if (el) { lo = key < lo ? key : lo; hi = key > hi ? key : hi; }
+    }
+    block_minmax_sum<NT>(lo, hi, dummy, sh);
+    const uint64_t diff = lo ^ hi;
+    if (diff == 0) return hi;  // one key left in play: it is the need-th (need == 1)
+    const int msb = 63 - __builtin_clzll(diff);
+    const int shift = msb > 7 ? msb - 7 : 0;
+    pmask = shift + 8 >= 64 ? 0 : ~((1ull << (shift + 8)) - 1);
+    prefix = hi & pmask;
+    for (int i = tid; i < 256; i += NT) sh.hist[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint64_t key = k[j];
+      if (key != 0 && (key > kZ) != lower_mode && (key & pmask) == prefix)
+        atomicAdd(&sh.hist[(key >> shift) & 255], 1);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      // lane l owns digits 255-4l .. 252-4l (top-down order); exclusive scan from the top
+      int c[4], sum = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { c[i] = sh.hist[255 - 4 * lane - i]; sum += c[i]; }
+      int incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+      }
+      int before = incl - sum;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (before < need && need <= before + c[i]) {
+          sh.sel_digit = 255 - 4 * lane - i;
+          sh.sel_above = before;
+          sh.sel_count = c[i];
+        }
+        before += c[i];
+      }
+    }
+    __syncthreads();
+    const int digit = sh.sel_digit, above = sh.sel_above, cnt = sh.sel_count;
+    __syncthreads();
+    prefix |= (uint64_t)digit << shift;
+    pmask |= (uint64_t)255 << shift;
+    need -= above;
+    if (shift == 0) return prefix;  // full key: a single (unique) key
+    if (cnt == need) {
+      // the whole bucket is in: the threshold is its smallest key (a real key, so `key >= T`
+      // never reaches below the eligible class)
+      uint64_t m = ~0ull, h = 0;
+      int d = 0;
+#pragma unroll
+      for (int j = 0; j < PER; ++j) {
+        const uint64_t key = k[j];
+        if (key != 0 && (key > kZ) != lower_mode && (key & pmask) == prefix) m = key < m ? key : m;
+      }
+      block_minmax_sum<NT>(m, h, d, sh);
+      return m;
+    }
+  }
+}
+
+template <int NT>
+__device__ int block_count_real(int local, SelectShared& sh) {
+  if (threadIdx.x == 0) sh.nreal = 0;
+  __syncthreads();
+  if (local) atomicAdd(&sh.nreal, local);
+  __syncthreads();
+  return sh.nreal;
+}
+
+// ---- stage 1: per-tile NMS + top-K candidates -------------------------------------------
+struct TileGeom {
+  int cg, th, tw;          // tile extent: channels, rows, columns
+  int ncg, nth, ntw;       // tiles per image along each
+  int r;                   // NMS radius (0 = no NMS), halo width
+  int apply_sigmoid;
+  int chan_fast;           // LDS fill order: 1 = channel fastest (NHWC views), 0 = column fastest
+};
+
+__global__ __launch_bounds__(kTileThreads) void tile_select(const float* __restrict__ heat, int64_t s0, int64_t s1,
+                                                            int64_t s2, int64_t s3, int C, int H, int W,
+                                                            const TileGeom g, int K, uint64_t* __restrict__ cand) {
+  extern __shared__ __attribute__((aligned(16))) float tile[];
+  __shared__ SelectShared sh;
+  const int b = blockIdx.y;
+  int t = blockIdx.x;
+  const int tx = t % g.ntw; t /= g.ntw;
+  const int ty = t % g.nth;
+  const int tc = t / g.nth;
+  const int c0 = tc * g.cg, y0 = ty * g.th, x0 = tx * g.tw;
+  const int nc = min(g.cg, C - c0), nh = min(g.th, H - y0), nw = min(g.tw, W - x0);
+  const int r = g.r;
+  const int LH = nh + 2 * r, LW = nw + 2 * r;
+  const float* base = heat + b * s0;
+
+  // tile + halo -> LDS [cc][yy][xx], sigmoid applied once per element; outside the image -inf
+  const int nl = nc * LH * LW;
+  for (int e = threadIdx.x; e < nl; e += kTileThreads) {
+    int cc, yy, xx;
+    if (g.chan_fast) {
+      cc = e % nc;
+      const int p = e / nc;
+      xx = p % LW;
+      yy = p / LW;
+    } else {
+      xx = e % LW;
+      const int p = e / LW;
+      yy = p % LH;
+      cc = p / LH;
+    }
+    const int y = y0 + yy - r, x = x0 + xx - r;
+    float v = -INFINITY;
+    if (y >= 0 && y < H && x >= 0 && x < W) {
+      v = base[(int64_t)(c0 + cc) * s1 + (int64_t)y * s2 + (int64_t)x * s3];
+      if (g.apply_sigmoid) v = sigmoidf_ref(v);
+    }
+    tile[(cc * LH + yy) * LW + xx] = v;
+  }
+  __syncthreads();
+
+  // NMS keys of this thread's elements (element e = tid + j * NT, column fastest)
+  const int ne = nc * nh * nw;
+  uint64_t k[kTilePer];
+#pragma unroll
+  for (int j = 0; j < kTilePer; ++j) {
+    const int e = threadIdx.x + j * kTileThreads;
+    k[j] = 0;
+    if (e < ne) {
+      const int xx = e % nw;
+      const int p = e / nw;
+      const int yy = p % nh;
+      const int cc = p / nh;
+      const float* row = tile + (cc * LH + yy + r) * LW + xx + r;
+      const float v = row[0];
+      float m = v;
+      if (r) {
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+          for (int dx = -1; dx <= 1; ++dx) m = fmaxf(m, row[dy * LW + dx]);
+      }
+      const float pv = (float)(m == v) * v;  // (hmax == h).float() * h (decode.py:252)
+      const uint32_t flat = (uint32_t)(((c0 + cc) * H + y0 + yy) * W + x0 + xx);
+      k[j] = make_key(pv, flat);
+    }
+  }
+  const int kt = min(K, ne);
+  const uint64_t T = block_select<kTileThreads, kTilePer>(k, kt, sh);
+  if (threadIdx.x == 0) sh.nout = 0;
+  __syncthreads();
+  uint64_t* out = cand + ((size_t)b * gridDim.x + blockIdx.x) * K;
+#pragma unroll
+  for (int j = 0; j < kTilePer; ++j)
+    if (k[j] != 0 && k[j] >= T) out[atomicAdd(&sh.nout, 1)] = k[j];
+  for (int i = kt + threadIdx.x; i < K; i += kTileThreads) out[i] = 0;
+}
+
+// ---- stage 2: merge candidate lists (K slots each) -> top K -----------------------------
 __device__ void bitonic_desc(uint64_t* a, int P) {
   for (int k = 2; k <= P; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < P; i += kSelThreads) {
-        int ixj = i ^ j;
+      for (int i = threadIdx.x; i < P; i += kMergeThreads) {
+        const int ixj = i ^ j;
         if (ixj > i) {
-          uint64_t x = a[i], y = a[ixj];
-          bool up = (i & k) == 0;  // this run ends descending
+          const uint64_t x = a[i], y = a[ixj];
+          const bool up = (i & k) == 0;  // this run ends descending
           if (up ? (x < y) : (x > y)) {
             a[i] = y;
             a[ixj] = x;
@@ -116,158 +331,193 @@ __device__ void bitonic_desc(uint64_t* a, int P) {
   }
 }
 
-__global__ __launch_bounds__(kSelThreads) void topk_kernel(const float* __restrict__ peaks, int64_t n, int K,
-                                                           float* __restrict__ out_score,
-                                                           int32_t* __restrict__ out_index) {
-  __shared__ int hist[kBins];
-  __shared__ uint64_t eq[kCap];
+struct MergeOut {
+  float* score;        // [B][K] (final level)
+  int32_t* index;      // [B][K]
+  int records;         // 1: also write detection records (DecodeParams)
+};
+
+__global__ __launch_bounds__(kMergeThreads) void merge_select(const uint64_t* __restrict__ in, int lists, int group,
+                                                              int K, uint64_t* __restrict__ next, int final_level,
+                                                              const MergeOut mo, const DecodeParams p) {
+  __shared__ SelectShared sh;
   __shared__ uint64_t top[kMaxK];
-  __shared__ int wsum[16];
-  __shared__ int sel_digit, sel_before, sel_count, n_top, n_eq;
-  const float* v = peaks + (size_t)blockIdx.x * n;
-  const int tid = threadIdx.x;
-
-  uint64_t prefix = 0, pmask = 0;
-  int need = K, shift = 64;
-  for (;;) {
-    const int nshift = shift > 11 ? shift - 11 : 0;
-    const int width = shift - nshift;
-    const int nb = 1 << width;
-    for (int i = tid; i < kBins; i += kSelThreads) hist[i] = 0;
-    __syncthreads();
-    const uint64_t dmask = (uint64_t)(nb - 1);
-    for (int64_t i = tid; i < n; i += kSelThreads) {
-      uint64_t key = make_key(v[i], (uint32_t)i);
-      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> nshift) & dmask], 1);
-    }
-    __syncthreads();
-    // bins ordered from the top: thread t owns top-order positions 2t, 2t+1
-    int d0 = nb - 1 - 2 * tid, d1 = d0 - 1;
-    int h0 = d0 >= 0 ? hist[d0] : 0;
-    int h1 = d1 >= 0 ? hist[d1] : 0;
-    int incl = block_scan_incl(h0 + h1, wsum);
-    int before = incl - h0 - h1;
-    if (d0 >= 0 && before < need && need <= before + h0) {
-      sel_digit = d0; sel_before = before; sel_count = h0;
-    }
-    if (d1 >= 0 && before + h0 < need && need <= before + h0 + h1) {
-      sel_digit = d1; sel_before = before + h0; sel_count = h1;
-    }
-    __syncthreads();
-    prefix |= (uint64_t)sel_digit << nshift;
-    pmask |= dmask << nshift;
-    need -= sel_before;
-    const int cnt = sel_count;
-    shift = nshift;
-    __syncthreads();
-    if (cnt <= kCap || shift == 0) break;
-  }
-
-  // collect: keys strictly above the prefix are in; keys equal to it compete for `need`
-  if (tid == 0) { n_top = 0; n_eq = 0; }
-  __syncthreads();
-  for (int64_t i = tid; i < n; i += kSelThreads) {
-    uint64_t key = make_key(v[i], (uint32_t)i);
-    uint64_t hi = key & pmask;
-    if (hi > prefix) top[atomicAdd(&n_top, 1)] = key;
-    else if (hi == prefix) eq[atomicAdd(&n_eq, 1)] = key;
-  }
-  __syncthreads();
-  const int ne = n_eq;
-  int P = 1;
-  while (P < ne) P <<= 1;
-  for (int i = ne + tid; i < P; i += kSelThreads) eq[i] = 0;
-  __syncthreads();
-  bitonic_desc(eq, P);
-  const int nt = n_top;  // == K - need
-  for (int i = tid; i < need; i += kSelThreads) top[nt + i] = eq[i];
-  __syncthreads();
-  int PK = 1;
-  while (PK < K) PK <<= 1;
-  for (int i = K + tid; i < PK; i += kSelThreads) top[i] = 0;
-  __syncthreads();
-  bitonic_desc(top, PK);
-  for (int i = tid; i < K; i += kSelThreads) {
-    uint64_t key = top[i];
-    out_score[(size_t)blockIdx.x * K + i] = unorder_bits((uint32_t)(key >> 32));
-    out_index[(size_t)blockIdx.x * K + i] = (int32_t)(0xFFFFFFFFu - (uint32_t)key);
-  }
-}
-
-int launch_topk(const float* peaks, int B, int64_t n, int K, float* score, int32_t* index, hipStream_t s) {
-  if (K < 1 || K > kMaxK || K > n) { set_error("topk: need 1 <= K <= min(1024, C*H*W)"); return 1; }
-  if (n >= (int64_t)0xFFFFFFFF) { set_error("topk: image too large"); return 1; }
-  hipLaunchKernelGGL(topk_kernel, dim3(B), dim3(kSelThreads), 0, s, peaks, n, K, score, index);
-  TV_HIP(hipGetLastError());
-  return 0;
-}
-
-// ---- detection records ------------------------------------------------------------------
-__global__ void records_kernel(const DecodeParams p, int64_t ss0, int64_t ss1, int64_t ss2, int64_t ss3,
-                               int64_t os0, int64_t os1, int64_t os2, int64_t os3, int64_t ds0, int64_t ds1,
-                               int64_t ds2, int64_t ds3) {
-  __shared__ int cnt;
-  const int b = blockIdx.x;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
-  const int hw = p.H * p.W;
+  __shared__ int cnt_thr;
+  const int b = blockIdx.y, grp = blockIdx.x;
+  const int l0 = grp * group, nl = min(group, lists - l0);
+  const uint64_t* src = in + ((size_t)b * lists + l0) * K;
+  const int n = nl * K;
+  uint64_t k[kMergePer];
   int local = 0;
-  for (int k = threadIdx.x; k < p.K; k += blockDim.x) {
-    const float score = p.score[(size_t)b * p.K + k];
-    const int idx = p.index[(size_t)b * p.K + k];
+#pragma unroll
+  for (int j = 0; j < kMergePer; ++j) {
+    const int e = threadIdx.x + j * kMergeThreads;
+    k[j] = e < n ? src[e] : 0;
+    local += k[j] != 0;
+  }
+  const int real = block_count_real<kMergeThreads>(local, sh);
+  const int kt = min(K, real);
+  const uint64_t T = block_select<kMergeThreads, kMergePer>(k, kt, sh);
+  if (threadIdx.x == 0) { sh.nout = 0; cnt_thr = 0; }
+  __syncthreads();
+  if (!final_level) {
+    uint64_t* out = next + ((size_t)b * gridDim.x + grp) * K;
+#pragma unroll
+    for (int j = 0; j < kMergePer; ++j)
+      if (k[j] != 0 && k[j] >= T) out[atomicAdd(&sh.nout, 1)] = k[j];
+    for (int i = kt + threadIdx.x; i < K; i += kMergeThreads) out[i] = 0;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < kMergePer; ++j)
+    if (k[j] != 0 && k[j] >= T) top[atomicAdd(&sh.nout, 1)] = k[j];
+  int P = 1;
+  while (P < K) P <<= 1;
+  for (int i = kt + threadIdx.x; i < P; i += kMergeThreads) top[i] = 0;
+  __syncthreads();
+  bitonic_desc(top, P);
+  int local_thr = 0;
+  for (int i = threadIdx.x; i < K; i += kMergeThreads) {
+    const uint64_t key = top[i];
+    const float score = unorder_bits((uint32_t)(key >> 32));
+    const int idx = (int)(0xFFFFFFFFu - (uint32_t)key);
+    if (mo.score) {
+      mo.score[(size_t)b * K + i] = score;
+      mo.index[(size_t)b * K + i] = idx;
+    }
+    if (!mo.records) continue;
+    // detection record (decode.py:204-234 / 71-98 field meaning)
+    const int hw = p.H * p.W;
     const int label = idx / hw;
     const int rem = idx - label * hw;
     const int iy = rem / p.W;
     const int ix = rem - iy * p.W;
-    float* r = p.records + ((size_t)b * p.K + k) * 10;
-    const float* sz = p.size + b * ss0 + iy * ss1 + ix * ss2;
+    float* rr = p.records + ((size_t)b * K + i) * 10;
+    const float* sz = p.size + b * p.size_st[0] + iy * p.size_st[1] + ix * p.size_st[2];
     float y, x;
     if (p.pos_mode == 0) {
-      const float* of = p.offset + b * os0 + iy * os1 + ix * os2;
+      const float* of = p.offset + b * p.offset_st[0] + iy * p.offset_st[1] + ix * p.offset_st[2];
       y = (float)(((double)p.ratio * (double)iy + (double)of[0]) / (double)p.in_h);
-      x = (float)(((double)p.ratio * (double)ix + (double)of[os3]) / (double)p.in_w);
+      x = (float)(((double)p.ratio * (double)ix + (double)of[p.offset_st[3]]) / (double)p.in_w);
     } else {
       y = (float)iy / (float)p.out_h;
       x = (float)ix / (float)p.out_w;
     }
     float depth = __builtin_nanf("");
     if (p.depth) {
-      float d = p.depth[b * ds0 + iy * ds1 + ix * ds2];
-      float sg = 1.0f / (1.0f + expf(-d));
+      const float d = p.depth[b * p.depth_st[0] + iy * p.depth_st[1] + ix * p.depth_st[2]];
+      const float sg = 1.0f / (1.0f + expf(-d));
       depth = p.depth_mode == 0 ? (1.0f / sg) - 1.0f : 1.0f / sg;
     }
-    r[0] = (float)label;
-    r[1] = score;
-    r[2] = y;
-    r[3] = x;
-    r[4] = sz[0];
-    r[5] = sz[ss3];
-    r[6] = depth;
-    r[7] = (float)idx;
+    rr[0] = (float)label;
+    rr[1] = score;
+    rr[2] = y;
+    rr[3] = x;
+    rr[4] = sz[0];
+    rr[5] = sz[p.size_st[3]];
+    rr[6] = depth;
+    rr[7] = (float)idx;
     if (p.aux) {
       const float* a = p.aux + b * p.aux_st[0] + label * p.aux_st[1] + iy * p.aux_st[3] + ix * p.aux_st[4];
-      r[8] = a[0];
-      r[9] = a[p.aux_st[2]];
+      rr[8] = a[0];
+      rr[9] = a[p.aux_st[2]];
     } else {
-      r[8] = r[9] = __builtin_nanf("");
+      rr[8] = rr[9] = __builtin_nanf("");
     }
-    local += score >= p.score_thr ? 1 : 0;
+    local_thr += score >= p.score_thr ? 1 : 0;
   }
-  atomicAdd(&cnt, local);
-  __syncthreads();
-  if (threadIdx.x == 0) p.counts[b] = cnt;
+  if (mo.records) {
+    if (local_thr) atomicAdd(&cnt_thr, local_thr);
+    __syncthreads();
+    if (threadIdx.x == 0) p.counts[b] = cnt_thr;
+  }
 }
 
-int launch_decode_records(const DecodeParams& p, hipStream_t s) {
-  const int64_t z[4] = {0, 0, 0, 0};
-  const int64_t* os = p.offset_st ? p.offset_st : z;
-  const int64_t* ds = p.depth_st ? p.depth_st : z;
-  hipLaunchKernelGGL(records_kernel, dim3(p.B), dim3(256), 0, s, p, p.size_st[0], p.size_st[1], p.size_st[2],
-                     p.size_st[3], os[0], os[1], os[2], os[3], ds[0], ds[1], ds[2], ds[3]);
+// ---- host side --------------------------------------------------------------------------
+namespace {
+
+TileGeom tile_geom(int C, int H, int W, int r, int apply_sigmoid, int chan_fast) {
+  TileGeom g{};
+  g.tw = std::min(W, 512);
+  g.cg = std::min(C, std::max(1, kTileElems / (g.tw * 4)));
+  g.th = std::min(H, std::max(1, kTileElems / (g.tw * g.cg)));
+  g.ncg = (C + g.cg - 1) / g.cg;
+  g.nth = (H + g.th - 1) / g.th;
+  g.ntw = (W + g.tw - 1) / g.tw;
+  g.r = r;
+  g.apply_sigmoid = apply_sigmoid;
+  g.chan_fast = chan_fast;
+  return g;
+}
+
+size_t tile_lds(const TileGeom& g) { return (size_t)g.cg * (g.th + 2 * g.r) * (g.tw + 2 * g.r) * sizeof(float); }
+
+// merge levels: lists per image at each level (level 0 = tiles)
+std::vector<int> merge_levels(int tiles, int K) {
+  const int group = std::max(1, kMergeCap / K);
+  std::vector<int> lv{tiles};
+  while (lv.back() > group) lv.push_back((lv.back() + group - 1) / group);
+  return lv;
+}
+
+}  // namespace
+
+size_t select_workspace_bytes(int B, int C, int H, int W, int K) {
+  const TileGeom g = tile_geom(C, H, W, 1, 1, 1);
+  const int tiles = g.ncg * g.nth * g.ntw;
+  const std::vector<int> lv = merge_levels(tiles, K);
+  // level i reads buffer i & 1 and writes buffer (i + 1) & 1; list counts only shrink, so
+  // buffer 0 is sized by level 0 and buffer 1 by level 1
+  const size_t b0 = (size_t)B * lv[0] * K * 8, b1 = lv.size() > 1 ? (size_t)B * lv[1] * K * 8 : 0;
+  return (b0 + 255) / 256 * 256 + (b1 + 255) / 256 * 256;
+}
+
+int launch_select(const float* heat, const int64_t st[4], int B, int C, int H, int W, int nms, int apply_sigmoid,
+                  int K, void* ws, size_t ws_bytes, float* score, int32_t* index, const DecodeParams* rec,
+                  hipStream_t s) {
+  const int64_t n = (int64_t)C * H * W;
+  if (K < 1 || K > kMaxK || K > n) { set_error("topk: need 1 <= K <= min(1024, C*H*W)"); return 1; }
+  if (n >= (int64_t)0xFFFFFFFF) { set_error("topk: image too large"); return 1; }
+  if (B == 0) return 0;
+  const TileGeom g = tile_geom(C, H, W, nms ? 1 : 0, apply_sigmoid, st[1] < st[3] ? 1 : 0);
+  const int tiles = g.ncg * g.nth * g.ntw;
+  const std::vector<int> lv = merge_levels(tiles, K);
+  if (ws_bytes < select_workspace_bytes(B, C, H, W, K)) { set_error("decode workspace too small"); return 1; }
+  if (tiles > 65535 || B > 65535) { set_error("decode: grid too large"); return 1; }
+  const size_t lds = tile_lds(g);
+  uint64_t* buf[2] = {(uint64_t*)ws, (uint64_t*)((char*)ws + ((size_t)B * lv[0] * K * 8 + 255) / 256 * 256)};
+  hipLaunchKernelGGL(tile_select, dim3(tiles, B), dim3(kTileThreads), lds, s, heat, st[0], st[1], st[2], st[3], C, H,
+                     W, g, K, buf[0]);
   TV_HIP(hipGetLastError());
+  const int group = std::max(1, kMergeCap / K);
+  MergeOut mo{score, index, rec ? 1 : 0};
+  DecodeParams p = rec ? *rec : DecodeParams{};
+  for (size_t i = 0; i < lv.size(); ++i) {
+    const int lists = lv[i];
+    const int groups = (lists + group - 1) / group;
+    const int fin = groups == 1;
+    uint64_t* in = buf[i & 1];
+    uint64_t* nxt = buf[(i + 1) & 1];
+    hipLaunchKernelGGL(merge_select, dim3(groups, B), dim3(kMergeThreads), 0, s, in, lists, group, K, nxt, fin, mo, p);
+    TV_HIP(hipGetLastError());
+    if (fin) break;
+  }
   return 0;
 }
 
+// heatmap_detect on a dense [B, n] map: C = 1, H = 1, W = n, no NMS, no sigmoid
+int launch_topk(const float* peaks, int B, int64_t n, int K, float* score, int32_t* index, hipStream_t s) {
+  if (n < 1 || n >= (int64_t)0x7FFFFFFF) { set_error("topk: bad row length"); return 1; }
+  const size_t need = select_workspace_bytes(B, 1, 1, (int)n, K);
+  void* ws = nullptr;
+  TV_HIP(hipMallocAsync(&ws, std::max<size_t>(need, 256), s));
+  const int64_t st[4] = {n, 0, 0, 1};
+  int rc = launch_select(peaks, st, B, 1, 1, (int)n, 0, 0, K, ws, need, score, index, nullptr, s);
+  TV_HIP(hipFreeAsync(ws, s));
+  return rc;
+}
+
+// ---- heatmap_detect()'s (index, label) as int64 ---------------------------------------------
 __global__ void index_split_kernel(const int32_t* __restrict__ flat, int n, int hw, int W,
                                    int64_t* __restrict__ index, int64_t* __restrict__ label) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -266,7 +266,6 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
       cu_count = ncu;
   }
-  if (const char* env = std::getenv("TV_CONV_HALO")) halo_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_C3_TW")) c3_tw_force = std::atoi(env) == 16 ? 16 : std::atoi(env) == 32 ? 32 : 0;
   if (const char* env = std::getenv("TV_CUS")) cu_count = std::max(8, std::min(cu_count, std::atoi(env)));
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
@@ -275,7 +274,6 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
   if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_S2_MINTILES")) s2_min_tiles = std::atoi(env);
-  if (const char* env = std::getenv("TV_SKIP_KINDS")) skip_kinds = std::atoi(env);
   if (const char* env = std::getenv("TV_C3_NI")) c3_ni_force = std::atoi(env) == 2 ? 2 : std::atoi(env) == 4 ? 4 : 0;
   if (const char* env = std::getenv("TV_C3_HALF_COST")) c3_half_cost = std::atoi(env);
   if (const char* env = std::getenv("TV_SLICES")) slices = std::max(1, std::min(kMaxSlices, std::atoi(env)));
@@ -427,7 +425,6 @@ int Engine::make_workspace(int B, Workspace* ws) {
   std::vector<size_t> ks_off(plan.ops.size(), 0);
   ws->use_pipe.assign(plan.ops.size(), 0);
   ws->kname.assign(plan.ops.size(), std::string());
-  ws->halo_tw.assign(plan.ops.size(), 0);
   ws->c3_tw.assign(plan.ops.size(), 0);
   ws->c3_grid.assign(plan.ops.size(), 0);
   ws->s2_grid.assign(plan.ops.size(), 0);
@@ -474,24 +471,6 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.mtiles = mt;
     }
     p.zero = zero_page;
-    if (const char* env = std::getenv("TV_ABLATE")) p.ablate = std::atoi(env);
-    // 3x3 / stride 1 / pad 1 single-input convs with whole channel blocks: halo-tile kernel
-    if (halo_mode && op.kind == OP_CONV && op.segs.size() == 1) {
-      const SegSpec& sg = op.segs[0];
-      const ConvSegment& cs = p.seg[0];
-      const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
-      if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand &&
-          cs.C % BK == 0 && cs.ldc % (16 / esz) == 0) {
-        const int t16 = halo_tiles(B, cs.H, cs.W, 16), t32 = halo_tiles(B, cs.H, cs.W, 32);
-        const int tw = t32 <= t16 ? 32 : 16;
-        const int mt = tw == 32 ? t32 : t16;
-        if ((long)mt * p.ntiles >= (halo_mode == 2 ? 1 : 32)) {
-          ws->halo_tw[i] = tw;
-          ws->use_pipe[i] = 0;
-          p.mtiles = mt;
-        }
-      }
-    }
     // persistent halo-tile 3x3 kernel (conv3x3.hip): 3x3 / stride 1 / pad 1, one input of 128
     // channels, fp16/bf16, 16-byte aligned channel slices, byte offsets within 2^31
     // A second segment is accepted when it is ResidualBlock's 1x1 conv_residual (128 channels,
@@ -537,7 +516,6 @@ int Engine::make_workspace(int B, Workspace* ws) {
         ws->c3_ni[i] = ni;
         ws->c3_res[i] = res;
         ws->c3_grid[i] = grid;
-        ws->halo_tw[i] = 0;
         ws->use_pipe[i] = 0;
         p.mtiles = mt;
       }
@@ -566,7 +544,6 @@ int Engine::make_workspace(int B, Workspace* ws) {
         p.mtiles = mt;
         ws->s2_grid[i] = grid;
         ws->use_pipe[i] = 0;
-        ws->halo_tw[i] = 0;
       }
     }
   }
@@ -619,7 +596,6 @@ int Engine::make_workspace(int B, Workspace* ws) {
     t.sy = op.sy;
     t.sx = op.sx;
     convt_schedule(t, cu_count);
-    if (const char* env = std::getenv("TV_CONVT_ABLATE")) t.ablate = std::atoi(env);
     ws->convt[i] = 1;
     ws->use_pipe[i] = 0;
   }
@@ -628,17 +604,6 @@ int Engine::make_workspace(int B, Workspace* ws) {
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
     for (size_t i = 0; i < plan.ops.size(); ++i)
       if (ws->use_pipe[i]) ws->params[i].ks = ws->dks + ks_off[i];
-  }
-  if (std::getenv("TV_STAMPS")) {  // diagnostics: per-block phase timestamps of pipelined convs
-    ws->stamps.assign(plan.ops.size(), nullptr);
-    for (size_t i = 0; i < plan.ops.size(); ++i) {
-      if (!ws->use_pipe[i] && !ws->c3_tw[i]) continue;
-      ConvParams& p = ws->params[i];
-      const size_t nb = ws->c3_tw[i] ? (size_t)ws->c3_grid[i] : (size_t)p.mtiles * p.ntiles;
-      TV_HIP(hipMalloc((void**)&ws->stamps[i], nb * kStampWords * 8));
-      TV_HIP(hipMemset(ws->stamps[i], 0, nb * kStampWords * 8));
-      p.stamps = ws->stamps[i];
-    }
   }
   TV_HIP(hipMalloc((void**)&ws->dparams, ws->params.size() * sizeof(ConvParams)));
   TV_HIP(hipMemcpy(ws->dparams, ws->params.data(), ws->params.size() * sizeof(ConvParams), hipMemcpyHostToDevice));
@@ -671,11 +636,6 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const OpSpec& op = plan.ops[i];
   char* base = (char*)ws->arena;
   if (stem_op >= 0 && op.kind == OP_PREP) return TV_OK;  // staging runs inside the stem kernel
-  if (skip_kinds) {  // what-if timing diagnostic (env TV_SKIP_KINDS): results are garbage
-    const int kind = (int)i == stem_op ? 8 : ws->head_fused[i] ? 32 : ws->convt[i] ? 2 : ws->s2_grid[i] ? 4
-                     : ws->c3_tw[i] ? 16 : (op.kind == OP_CONV || op.kind == OP_CONVT_ADD) && !ws->head_skip[i] ? 1 : 0;
-    if (skip_kinds & kind) return TV_OK;
-  }
   if ((int)i == stem_op) {
     StemParams sp{};
     sp.input = input;
@@ -688,7 +648,6 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     sp.N = op.N;
     sp.weight = packed[i].w;
     sp.bias = packed[i].bias;
-    if (const char* env = std::getenv("TV_STEM_ABLATE")) sp.ablate = std::atoi(env);
     return launch_stem(sp, dtype, cu_count, s);
   }
   if (op.kind == OP_PREP) {
@@ -730,7 +689,6 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
                                            ws->c3_res[i], ws->c3_ni[i])
-           : ws->halo_tw[i] ? launch_conv_halo(p, ws->dparams + i, p.out, dtype, out_f32, ws->halo_tw[i], s)
            : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
                              : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
   if (rc) return rc;
@@ -865,7 +823,6 @@ const char* Engine::op_kernel(int B, size_t i) {
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ">";
-      else if (ws->halo_tw[i]) name = std::string("tv::halo::conv_halo<") + t + ", " + o + ", " + std::to_string(ws->halo_tw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";
     }
@@ -899,20 +856,6 @@ int Engine::profile(const void* input, int input_u8, int B, float* out, hipStrea
       flops[i] = plan.ops[i].flops * B;
     }
     *n_ops = (int)n;
-    if (const char* path = std::getenv("TV_STAMPS")) {
-      for (size_t i = 0; i < n && i < ws->stamps.size(); ++i) {
-        if (!ws->stamps[i]) continue;
-        const ConvParams& p = ws->params[i];
-        const size_t nb = ws->c3_tw[i] ? (size_t)ws->c3_grid[i] : (size_t)p.mtiles * p.ntiles;
-        std::vector<unsigned long long> h(nb * kStampWords);
-        TV_HIP(hipMemcpy(h.data(), ws->stamps[i], h.size() * 8, hipMemcpyDeviceToHost));
-        const std::string f = std::string(path) + "_" + std::to_string(i) + ".bin";
-        if (FILE* fp = std::fopen(f.c_str(), "wb")) {
-          std::fwrite(h.data(), 8, h.size(), fp);
-          std::fclose(fp);
-        }
-      }
-    }
   }
   for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;

@@ -34,7 +34,6 @@ struct Workspace {
   std::vector<ConvParams> params;   // per op (host copy)
   ConvParams* dparams = nullptr;    // per op (device copy)
   std::vector<int> use_pipe;        // per op: 1 = conv_pipe (256-pixel tiles), 0 = conv_igemm
-  std::vector<int> halo_tw;         // per op: > 0 = conv_halo with this tile width (overrides use_pipe)
   std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
   std::vector<int> c3_res;          // per op: 1 = conv3x3 with the 1x1 residual segment (RES)
   std::vector<int> c3_ni;           // per op: channel fragments per wave (4: 128-channel tiles, 2: 64)
@@ -44,7 +43,6 @@ struct Workspace {
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
   std::vector<ConvTParams> tparams; // per op: convt.hip launch parameters
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
-  std::vector<unsigned long long*> stamps;  // diagnostics (env TV_STAMPS), per op
   std::vector<std::string> kname;   // per op: kernel instance name (diagnostics), filled lazily
 };
 
@@ -59,8 +57,6 @@ struct Engine {
   int pipe_mode = 1;           // -1 auto (>= 256 tiles), 0 never, 1 whenever representable (env TV_CONV_PIPE)
   int c3_tw_force = 0;         // conv3x3 tile width override (env TV_C3_TW = 16 / 32)
   int s2_min_tiles = -1;       // stride-2 halo kernel from this many tiles (env TV_S2_MINTILES; -1 = cu_count)
-  int skip_kinds = 0;          // timing diagnostic only (env TV_SKIP_KINDS): launch families to skip —
-                               // 1 implicit GEMM, 2 ConvT, 4 stride-2 halo, 8 stem, 16 3x3 halo, 32 heads
   int c3_ni_force = 0;         // conv3x3 channel tile: 0 = by grid rounds, 2 / 4 forced (env TV_C3_NI)
   int c3_half_cost = 55;       // cost of a 64-channel half tile in % of a full one (env TV_C3_HALF_COST, 0 = never)
   int conv3_min_pix = 1;       // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)
@@ -72,7 +68,6 @@ struct Engine {
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1
-  int halo_mode = 0;           // 1 enables the halo-tile 3x3 kernel, 2 forces it (env TV_CONV_HALO)
   // concurrent slices: a batch of >= slices * slice_min frames runs as `slices` near-equal parts,
   // the first on the caller's stream and the others on side streams (fork / join events), so one
   // slice's latency-bound small layers and grid tails overlap another's large layers

@@ -255,7 +255,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
           const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
           const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
           const int ch = 32 * i + 16 * m + 8 * lh;
-          if (ok && ch < p.N && !(p.ablate & 1)) gstore16(dst + ch, make_uint4(r0[0], r1[0], r0[1], r1[1]));
+          if (ok && ch < p.N) gstore16(dst + ch, make_uint4(r0[0], r1[0], r0[1], r1[1]));
         }
       }
     }
@@ -273,12 +273,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // tile k of this block: t = t0 + k*G, E buffer k % 2, window of tile k+1 in set (k+1) % 2
   auto tile = [&](int t, int eb, unsigned (&raw_next)[NS], unsigned (&raw_k2)[NS]) __attribute__((always_inline)) {
     const int tn = t + G, tn2 = t + 2 * G;
-    if (tn2 < ntot && !(p.ablate & 4)) load_window(tn2, raw_k2);  // tile k's set: already consumed
-    if (!(p.ablate & 2)) mfma_row(eb, std::integral_constant<int, 0>{});
+    if (tn2 < ntot) load_window(tn2, raw_k2);  // tile k's set: already consumed
+    mfma_row(eb, std::integral_constant<int, 0>{});
     epilogue(t, std::integral_constant<int, 0>{});
-    if (!(p.ablate & 2)) mfma_row(eb, std::integral_constant<int, 1>{});
+    mfma_row(eb, std::integral_constant<int, 1>{});
     epilogue(t, std::integral_constant<int, 1>{});
-    if (tn < ntot && !(p.ablate & 4)) {
+    if (tn < ntot) {
       store_window(tn, raw_next);  // N is free: its last reader (expand) finished before the last barrier
       lds_barrier();
       expand(eb ^ 1);  // E[eb ^ 1] was last read by the previous tile's MFMAs

@@ -97,6 +97,10 @@ def gen_models(rcfg, rnet, rdla, rdec):
         for thr in (0.05, 0.3):
             dets = rdec.decode(pred, mc, 20, thr)
             out[f"decode_thr{thr}"] = _pack_dets(dets, 20, has_depth=pred.depth is not None)
+        # the bench's decode (K=100) with no threshold cut: every top-100 peak's record, so the
+        # fp16/bf16 paths' peak-set agreement and box error are measured against the reference
+        out["decode_k100"] = _pack_dets(rdec.decode(pred, mc, 100, 0.0), 100, has_depth=pred.depth is not None)
+        out["decode_k100_index"] = _flat_peaks(rdec, pred.heatmap, 100)
         if oc.train_keypoints:
             kd = rdec.decode_keypoints(pred, mc, oc, np.eye(3), n_detections=10, keypoint_n_detections=50,
                                        score_threshold=0.05, keypoint_score_threshold=0.05,
@@ -123,6 +127,15 @@ def _pack_dets(dets, K, has_depth):
             rec[b, i, 6] = d.depth if (has_depth and d.depth is not None) else np.nan
             rec[b, i, 7] = 1.0
     return rec
+
+
+def _flat_peaks(rdec, heatmap, K):
+    """[B, K] int64 flat peak indices (label*H*W + y*W + x) of the reference's own
+    sigmoid -> heatmap_nms -> heatmap_detect chain (decode.py:182-184), in its order."""
+    import torch.nn.functional as F
+    H, W = heatmap.shape[2:]
+    idx, lab, _ = rdec.heatmap_detect(rdec.heatmap_nms(F.sigmoid(heatmap), 3), K)
+    return (lab * H * W + idx[..., 0] * W + idx[..., 1]).numpy()
 
 
 def _pack_kp_dets(dets, K, oc):

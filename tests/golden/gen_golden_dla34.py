@@ -34,7 +34,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from recipe import DLA34_CASES, seeded_state_dict, seeded_input  # noqa: E402
-from gen_golden import _import_reference, object_config_for, _pack_dets  # noqa: E402
+from gen_golden import _import_reference, object_config_for, _pack_dets, _pack_kp_dets, _flat_peaks  # noqa: E402
 from oracle.ref_dla34 import deform_conv2d  # noqa: E402
 
 
@@ -98,6 +98,15 @@ def main():
         for thr in (0.05, 0.3):
             out[f"decode_thr{thr}"] = _pack_dets(rdec.decode(pred, mc, 20, thr), 20,
                                                  has_depth=pred.depth is not None)
+        out["decode_k100"] = _pack_dets(rdec.decode(pred, mc, 100, 0.0), 100, has_depth=pred.depth is not None)
+        out["decode_k100_index"] = _flat_peaks(rdec, pred.heatmap, 100)
+        if oc.train_keypoints:
+            # the node's call (centernet_node.py:106-116: 10 objects, 50 keypoints) at thresholds
+            # low enough for seeded weights to produce matches
+            kd = rdec.decode_keypoints(pred, mc, oc, np.eye(3), n_detections=10, keypoint_n_detections=50,
+                                       score_threshold=0.05, keypoint_score_threshold=0.05,
+                                       keypoint_angle_threshold=0.3)
+            out["decode_keypoints"] = _pack_kp_dets(kd, 10, oc)
         out["weight_checksums"] = np.array([[float(v.double().sum()), float(v.double().abs().sum())]
                                             if v.dtype.is_floating_point else [float(v), 0.0]
                                             for v in sd.values()])

@@ -49,6 +49,10 @@ DLA34_CASES = [
     # the BASELINE geometry (480x640) with the north-star DLA34 heads [4, 4, 8, 2, 2]
     dict(name="b1_480x640_kp", in_h=480, in_w=640, batch=1, seed=202,
          objects={"n_labels": 4, "keypoints_per_label": 1}),
+    # the production node's configuration (centernet_node.py:46 with samples_torpedo.py:4-82):
+    # 360x640, 4 labels x 1 keypoint; ida_up's pad_to_match shifts one row (92 -> 90, a14)
+    dict(name="b1_360x640_kp", in_h=360, in_w=640, batch=1, seed=203,
+         objects={"n_labels": 4, "keypoints_per_label": 1}),
 ]
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)

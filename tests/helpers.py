@@ -19,6 +19,19 @@ def models_index():
     return _MODELS
 
 
+_MEASURED = {}
+
+
+def record_measurement(key, value):
+    """Collect measured drift (env TV_PARITY_OUT = JSON path) so tolerances can be set from
+    numbers measured on MI355X; profiles/r2/parity_lowp.json is such a file."""
+    _MEASURED[key] = value
+    out = os.environ.get("TV_PARITY_OUT")
+    if out:
+        with open(out, "w") as f:
+            json.dump(_MEASURED, f, indent=1, sort_keys=True)
+
+
 def golden(name):
     return np.load(os.path.join(GOLDEN, name if name.endswith(".npz") else name + ".npz"))
 

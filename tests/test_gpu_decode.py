@@ -135,3 +135,60 @@ def test_saturated_sigmoid_ties_are_peaks():
     ref = oracle.heatmap_nms(torch.sigmoid(logits), 3)
     got = tv.heatmap_nms(torch.sigmoid(logits).cuda(), 3).cpu()
     assert torch.equal(got, ref) and int((ref == 1.0).sum()) == 2
+
+
+def _tie_rule_topk(x, K):
+    """[B, n] -> (score, flat) of the top K with ties to the smaller flat index (the kernel's
+    deterministic rule; torch.topk leaves tie order unspecified, decode.py:269)."""
+    out_s, out_i = [], []
+    for row in x:
+        order = np.lexsort((np.arange(row.size), -row.astype(np.float64)))[:K]
+        out_s.append(row[order])
+        out_i.append(order)
+    return np.stack(out_s), np.stack(out_i)
+
+
+@pytest.mark.parametrize("shape,K", [((1, 4, 400, 400), 1024),   # 80 tiles > 16 per merge: two merge levels
+                                     ((2, 80, 64, 64), 100),     # channel-group tiles
+                                     ((3, 1, 1, 5000), 7),       # one row wider than a column band
+                                     ((64, 4, 120, 160), 100)])  # the bench's decode shape
+def test_topk_multi_tile_matches_sort(shape, K):
+    from tauv_vision_amd import heatmap_detect, heatmap_nms
+    g = torch.Generator().manual_seed(sum(shape) + K)
+    x = torch.randn(shape, generator=g)
+    nms = heatmap_nms(torch.sigmoid(x).cuda(), 3)
+    idx, lab, score = heatmap_detect(nms, K)
+    B, C, H, W = shape
+    ref_s, ref_i = _tie_rule_topk(nms.cpu().numpy().reshape(B, -1), K)
+    flat = (lab * H * W + idx[..., 0] * W + idx[..., 1]).cpu().numpy()
+    np.testing.assert_array_equal(score.cpu().numpy(), ref_s)
+    np.testing.assert_array_equal(flat, ref_i)
+
+
+def test_fused_decode_matches_oracle_large_batch():
+    """tv_decode (fused NMS + selection + records) at B=64 on continuous random heads vs the CPU
+    oracle decode (K=100, every record: thr 0) — peak cells, scores and boxes."""
+    import tauv_vision_amd as tv
+    from tauv_vision_amd.decode import DeviceDecoder
+    g = torch.Generator().manual_seed(77)
+    B, C, H, W, K = 64, 4, 120, 160, 100
+    logits = torch.randn((B, C, H, W), generator=g) * 3.0
+    size = torch.randn((B, H, W, 2), generator=g) * 10.0
+    offset = torch.rand((B, H, W, 2), generator=g)
+    dec = DeviceDecoder(B, C, H, W, K, torch.device("cuda"))
+    rec, cnt = dec(logits.cuda(), size.cuda(), offset.cuda(), None, 0, 4, 480, 640, 0.0)
+    rec = rec.cpu().numpy()
+    assert (cnt.cpu().numpy() == K).all()
+    sig = torch.sigmoid(logits)
+    nms = oracle.heatmap_nms(sig, 3).reshape(B, -1).numpy()
+    ref_s, ref_i = _tie_rule_topk(nms, K)
+    np.testing.assert_array_equal(rec[..., 7].astype(np.int64), ref_i)
+    np.testing.assert_allclose(rec[..., 1], ref_s, rtol=0, atol=1e-6)  # device expf vs CPU sigmoid
+    lab, rem = ref_i // (H * W), ref_i % (H * W)
+    iy, ix = rem // W, rem % W
+    bi = np.arange(B)[:, None]
+    np.testing.assert_array_equal(rec[..., 0], lab)
+    np.testing.assert_array_equal(rec[..., 4], size.numpy()[bi, iy, ix, 0])
+    np.testing.assert_array_equal(rec[..., 5], size.numpy()[bi, iy, ix, 1])
+    y = ((4.0 * iy + offset.numpy()[bi, iy, ix, 0].astype(np.float64)) / 480).astype(np.float32)
+    np.testing.assert_array_equal(rec[..., 2], y)

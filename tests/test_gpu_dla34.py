@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import golden, dla34_index, dla34_state_dict, dla34_input
+from helpers import golden, dla34_index, dla34_state_dict, dla34_input, record_measurement
 
 pytestmark = pytest.mark.gpu
 
@@ -35,7 +35,8 @@ def build(name, precision):
     return model, oc, mc, case
 
 
-def _cmp(pred, g, tol):
+def _cmp(pred, g, tol, key=None):
+    meas = {}
     for f in FIELDS:
         t = getattr(pred, f)
         if f not in g.files:
@@ -46,6 +47,9 @@ def _cmp(pred, g, tol):
         assert got.shape == ref.shape, (f, got.shape, ref.shape)
         scale = max(1.0, float(np.abs(ref).max()))
         err = float(np.abs(got - ref).max())
+        meas[f] = err / scale
+        if key:
+            record_measurement(key, meas)
         assert err <= tol * scale, f"{f}: max|err| {err:.3e} > {tol} * {scale:.3g}"
 
 
@@ -65,6 +69,17 @@ def test_dla34_fp32_matches_reference(name):
             for i, d in enumerate(got[b]):
                 assert int(d.label) == int(ref[b, i, 0])
                 np.testing.assert_allclose([float(d.score), d.y, d.x, d.h, d.w], ref[b, i, 1:6], atol=1e-4, rtol=1e-4)
+    if "decode_keypoints" in g.files:  # the node's decode_keypoints call (centernet_node.py:106-116)
+        kd = tv.decode_keypoints(pred, mc, oc, np.eye(3), 10, 50, 0.05, 0.05, 0.3)
+        ref = g["decode_keypoints"]
+        for b in range(ref.shape[0]):
+            assert len(kd[b]) == int(np.nansum(ref[b, :, 6]))
+            for i, d in enumerate(kd[b]):
+                row = [d.label, d.score, d.y, d.x, d.h, d.w, 1.0]
+                for j in range(len(d.keypoints)):
+                    row += ([np.nan] * 5 if d.keypoints[j] is None else
+                            [*d.keypoints[j], d.keypoint_scores[j], *d.keypoint_affinities[j]])
+                np.testing.assert_allclose(np.array(row, dtype=np.float64), ref[b, i], atol=1e-4, rtol=1e-4)
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
@@ -73,7 +88,7 @@ def test_dla34_low_precision(name, precision):
     model, oc, mc, case = build(name, precision)
     with torch.no_grad():
         pred = model(dla34_input(name).cuda())
-    _cmp(pred, golden(f"dla34_{name}"), TOL[precision])
+    _cmp(pred, golden(f"dla34_{name}"), TOL[precision], key=f"dla34/{name}/{precision}")
 
 
 def test_dla34_u8_frames_and_batch_independence():

@@ -9,7 +9,8 @@ import pytest
 import torch
 
 import oracle
-from helpers import golden, models_index, case_by_name, case_state_dict, case_input, case_flags, keypoint_owner
+from helpers import golden, models_index, case_by_name, case_state_dict, case_input, case_flags, keypoint_owner, \
+    record_measurement
 
 pytestmark = pytest.mark.gpu
 
@@ -38,7 +39,8 @@ def build(name, precision):
     return model, oc, mc, case
 
 
-def _cmp(pred, g, tol):
+def _cmp(pred, g, tol, key=None):
+    meas = {}
     for f in FIELDS:
         t = getattr(pred, f)
         if f not in g.files:
@@ -49,6 +51,9 @@ def _cmp(pred, g, tol):
         assert got.shape == ref.shape, (f, got.shape, ref.shape)
         scale = max(1.0, float(np.abs(ref).max()))
         err = float(np.abs(got - ref).max())
+        meas[f] = err / scale
+        if key:
+            record_measurement(key, meas)
         assert err <= tol * scale, f"{f}: max|err| {err:.3e} > {tol} * {scale:.3g}"
 
 
@@ -89,7 +94,7 @@ def test_forward_fp32_full_size_r18():
 def test_forward_low_precision(name, precision):
     model, oc, mc, case = build(name, precision)
     pred = model(case_input(name).cuda())
-    _cmp(pred, golden(f"model_{name}"), TOL[precision])
+    _cmp(pred, golden(f"model_{name}"), TOL[precision], key=f"forward/{name}/{precision}")
 
 
 @pytest.mark.parametrize("name", ["r18_c16_b2_96x128", "torpedo_c16_b1_360x640"])

@@ -69,6 +69,26 @@ def _check_records(got, ref, has_depth):
             np.testing.assert_array_equal(np.array(row, dtype=np.float64), ref[b, i, :7])
 
 
+def _check_detcmp_self(g):
+    """tests/golden/detcmp.py on the reference's own records: full agreement at any drift."""
+    from detcmp import peak_parity
+    ref = g["decode_k100"]
+    B, K = g["decode_k100_index"].shape
+    rec = np.zeros((B, K, 10))
+    rec[..., :6] = ref[..., :6]
+    rec[..., 7] = g["decode_k100_index"]
+    for tol in (1e-6, 1e-3):
+        pp = peak_parity(rec, g["heatmap"], g["decode_k100_index"], ref, tol)
+        assert pp["agreement"] == 1.0 and pp["determined_found"] == pp["determined"] and pp["extra_ok"]
+        assert pp["max_score_err"] == 0.0 and pp["max_box_err"] == 0.0
+    # a swapped-out determined peak is caught
+    if K > 1:
+        bad = rec.copy()
+        bad[0, 0, 7] = -1
+        pp = peak_parity(bad, g["heatmap"], g["decode_k100_index"], ref, 1e-9)
+        assert pp["determined_found"] == pp["determined"] - 1 and not pp["extra_ok"]
+
+
 @pytest.mark.parametrize("name", [c for c in models_index()])
 def test_forward_golden(name):
     case = case_by_name(name)
@@ -88,6 +108,9 @@ def test_forward_golden(name):
     for thr in (0.05, 0.3):
         got = oracle.decode(pred, case["in_h"], case["in_w"], case["downsamples"], 20, thr)
         _check_records(got, g[f"decode_thr{thr}"], has_depth=pred.depth is not None)
+    got = oracle.decode(pred, case["in_h"], case["in_w"], case["downsamples"], 100, 0.0)
+    _check_records(got, g["decode_k100"], has_depth=pred.depth is not None)
+    _check_detcmp_self(g)
     if case_flags(case)["keypoints"]:
         ratio = 2 ** case["downsamples"]
         kd = oracle.decode_keypoints(pred, case["in_h"] // ratio, case["in_w"] // ratio, keypoint_owner(case),
@@ -130,6 +153,9 @@ def test_dla34_forward_golden(name):
                                        err_msg=f)
         else:
             assert t is None
+    flat = {int(i) for i in g["decode_k100_index"][0]}
+    assert len(flat) == 100
+    _check_detcmp_self(g)
 
 
 def test_deform_conv2d_kat():

@@ -159,7 +159,9 @@ __device__ uint64_t block_select(const uint64_t (&k)[PER], int need, SelectShare
     if (diff == 0) return hi;  // one key left in play: it is the need-th (need == 1)
     const int msb = 63 - __builtin_clzll(diff);
     const int shift = msb > 7 ? msb - 7 : 0;
-    pmask = shift + 8 >= 64 ? 0 : ~((1ull << (shift + 8)) - 1);
+    // bits above the window are shared by every key in play; bits fixed by earlier passes may
+    // reach into the window (a narrow final range) and stay fixed
+    pmask |= shift + 8 >= 64 ? 0 : ~((1ull << (shift + 8)) - 1);
     prefix = hi & pmask;
     for (int i = tid; i < 256; i += NT) sh.hist[i] = 0;
     __syncthreads();
@@ -308,7 +310,8 @@ __global__ __launch_bounds__(kTileThreads) void tile_select(const float* __restr
 #pragma unroll
   for (int j = 0; j < kTilePer; ++j)
     if (k[j] != 0 && k[j] >= T) out[atomicAdd(&sh.nout, 1)] = k[j];
-  for (int i = kt + threadIdx.x; i < K; i += kTileThreads) out[i] = 0;
+  __syncthreads();
+  for (int i = sh.nout + threadIdx.x; i < K; i += kTileThreads) out[i] = 0;
 }
 
 // ---- stage 2: merge candidate lists (K slots each) -> top K -----------------------------
@@ -365,7 +368,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_select(const uint64_t* __
 #pragma unroll
     for (int j = 0; j < kMergePer; ++j)
       if (k[j] != 0 && k[j] >= T) out[atomicAdd(&sh.nout, 1)] = k[j];
-    for (int i = kt + threadIdx.x; i < K; i += kMergeThreads) out[i] = 0;
+    __syncthreads();
+    for (int i = sh.nout + threadIdx.x; i < K; i += kMergeThreads) out[i] = 0;
     return;
   }
 #pragma unroll
@@ -373,7 +377,8 @@ __global__ __launch_bounds__(kMergeThreads) void merge_select(const uint64_t* __
     if (k[j] != 0 && k[j] >= T) top[atomicAdd(&sh.nout, 1)] = k[j];
   int P = 1;
   while (P < K) P <<= 1;
-  for (int i = kt + threadIdx.x; i < P; i += kMergeThreads) top[i] = 0;
+  __syncthreads();
+  for (int i = sh.nout + threadIdx.x; i < P; i += kMergeThreads) top[i] = 0;
   __syncthreads();
   bitonic_desc(top, P);
   int local_thr = 0;

@@ -3,8 +3,9 @@ made by the reference module (tests/golden/gen_golden_dla34.py; DCNv2 = the orac
 torchvision restatement, parity unpinned for that function only).
 
 fp32 (exact-f32 MFMA, BN folded): every Prediction tensor within 1e-4 * max(1, |ref|max).
-fp16 / bf16 (throughput modes): 3e-2 / 1.5e-1 of the tensor's range — DCN offsets are
-produced in the compute dtype, so sampling positions carry its rounding.
+fp16 / bf16 (throughput modes): 6e-4 / 4e-3 x max(1, |ref|max), ~3x the largest drift
+measured on MI355X (profiles/r2/parity_lowp.json: fp16 <= 2.0e-4, bf16 <= 1.4e-3; DCN offsets
+are produced in the compute dtype, so sampling positions carry its rounding).
 """
 import numpy as np
 import pytest
@@ -16,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 FIELDS = ["heatmap", "keypoint_heatmap", "keypoint_affinity", "size", "offset", "roll_bin", "roll_offset",
           "pitch_bin", "pitch_offset", "yaw_bin", "yaw_offset", "depth"]
-TOL = {"fp32": 1e-4, "fp16": 3e-2, "bf16": 1.5e-1}
+TOL = {"fp32": 1e-4, "fp16": 6e-4, "bf16": 4e-3}
 
 
 def build(name, precision):

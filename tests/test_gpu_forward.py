@@ -2,7 +2,8 @@
 
 fp32 mode (exact-f32 MFMA; BN folded at load): every Prediction tensor within
 1e-4 * max(1, |ref|max) of the reference PyTorch-CPU output. fp16 / bf16 modes are the
-throughput modes; their tolerance is stated per test (relative to the tensor's range).
+throughput modes: ~3x the largest drift measured on MI355X over these cases
+(profiles/r2/parity_lowp.json: fp16 <= 5.9e-4, bf16 <= 5.0e-3 of max(1, |ref|max)).
 """
 import numpy as np
 import pytest
@@ -16,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 FIELDS = ["heatmap", "keypoint_heatmap", "keypoint_affinity", "size", "offset", "roll_bin", "roll_offset",
           "pitch_bin", "pitch_offset", "yaw_bin", "yaw_offset", "depth"]
-TOL = {"fp32": 1e-4, "fp16": 2e-2, "bf16": 1e-1}
+TOL = {"fp32": 1e-4, "fp16": 2e-3, "bf16": 1.5e-2}
 
 
 def build(name, precision):

@@ -45,9 +45,13 @@ typedef enum tv_dtype { TV_F32 = 0, TV_F16 = 1, TV_BF16 = 2 } tv_dtype;
  * TV_ARCH_CENTERNET = Centernet(DLABackbone(heights, channels, downsamples)) (centernet.py:32-92,
  * dla.py:393-416); TV_ARCH_DLA34 = CenterpointDLA34 (centerpoint_dla.py:544-578: DLA-34 base,
  * DLAUp/IDAUp with DCNv2, down ratio 4, head_conv 256; n_levels/heights/channels/downsamples
- * are ignored). */
+ * are ignored); TV_ARCH_PROTONET = the YOLACT protonet Masknet (masknet.py:8-55): channels[0] =
+ * feature_depth, head_channels[0] = n_prototype_masks, (in_h, in_w) = the fpn[0] feature size;
+ * tv_engine_forward takes fpn[0] as fp32 NCHW [B, feature_depth, in_h, in_w] and writes the
+ * prototypes as fp32 NHWC [B, 4 in_h, 4 in_w, out_cpad]. */
 #define TV_ARCH_CENTERNET 0
 #define TV_ARCH_DLA34 1
+#define TV_ARCH_PROTONET 2
 typedef struct tv_model_desc {
   int32_t n_levels;          /* len(backbone_heights) */
   int32_t heights[8];        /* backbone_heights */
@@ -145,16 +149,35 @@ int tv_decode(const float* heat, const int64_t heat_strides[4], const float* siz
  *   (anchor_batch 1 broadcasts like the reference's [1,A,4] anchors), out [B,A,4]. */
 int tv_yolact_box_decode(const float* box_encoding, const float* anchor, int32_t B, int32_t A, int32_t anchor_batch,
                          float variance0, float variance1, float* box, void* stream);
+/* box_encode (boxes.py:45-53): box [B,A,4] (y, x, h, w), anchor [anchor_batch,A,4] -> encodings [B,A,4]. */
+int tv_yolact_box_encode(const float* box, const float* anchor, int32_t B, int32_t A, int32_t anchor_batch,
+                         float variance0, float variance1, float* box_encoding, void* stream);
 /* nms (nms.py:7-29): class-agnostic fast NMS of batch 0 — classification [A, C+1] logits and
  * box [A, 4] of batch 0; writes the kept anchor indices (descending confidence) to det[<= top_k]
- * (int64) and their number to *n_det (device int32). A <= 8192. */
+ * (int64) and their number to *n_det (device int32). Any anchor count; the sort workspace is
+ * allocated stream-ordered (hipMallocAsync) — use the batched entry point under graph capture. */
 int tv_yolact_fast_nms(const float* classification, int32_t A, int32_t n_classes_with_bg, const float* box,
                        int32_t top_k, float iou_threshold, float confidence_threshold, int64_t* det, int32_t* n_det,
                        void* stream);
-/* assemble_mask (masks.py:8-21): prototypes [K,H,W], coefficients [n,K], box [n,4] (y, x, h, w
- * normalised) or NULL -> mask [n,H,W] = sigmoid(coeff . proto) x inclusive box mask. */
-int tv_yolact_assemble_mask(const float* mask_prototype, int32_t K, int32_t H, int32_t W, const float* mask_coeff,
-                            const float* box, int32_t n, float* mask, void* stream);
+/* The same for B images at once (the reference's nms applied to every image of a batch):
+ * classification [B,A,C+1], box [B,A,4] -> det [B][min(top_k, A)] int64 (row b: n_det[b] kept
+ * indices), n_det [B] int32; workspace of tv_yolact_nms_workspace_size() bytes. */
+int tv_yolact_nms_workspace_size(int32_t B, int32_t A, int32_t top_k, int64_t* bytes);
+int tv_yolact_fast_nms_batched(const float* classification, int32_t B, int32_t A, int32_t n_classes_with_bg,
+                               const float* box, int32_t top_k, float iou_threshold, float confidence_threshold,
+                               int64_t* det, int32_t* n_det, void* workspace, int64_t workspace_bytes, void* stream);
+/* assemble_mask (masks.py:8-21): prototypes [K,H,W] at element strides proto_strides (k, y, x) —
+ * contiguous NCHW or the protonet's NHWC output view —, coefficients [n,K], box [n,4] (y, x, h, w
+ * normalised) or NULL -> mask [n,H,W] = sigmoid(coeff . proto) x inclusive box mask. K <= 40. */
+int tv_yolact_assemble_mask(const float* mask_prototype, const int64_t proto_strides[3], int32_t K, int32_t H,
+                            int32_t W, const float* mask_coeff, const float* box, int32_t n, float* mask,
+                            void* stream);
+/* The same for B images: prototypes at strides (b, k, y, x), coefficients [B][n_max][K], boxes
+ * [B][n_max][4] or NULL, counts [B] (device int32, detections per image; NULL = n_max) ->
+ * masks [B][n_max][H][W] (rows d >= counts[b] untouched). */
+int tv_yolact_assemble_masks(const float* mask_prototype, const int64_t proto_strides[4], int32_t B, int32_t K,
+                             int32_t H, int32_t W, const float* mask_coeff, const float* box, const int32_t* counts,
+                             int32_t n_max, float* mask, void* stream);
 
 const char* tv_last_error(void);
 const char* tv_version(void);

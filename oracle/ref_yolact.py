@@ -8,6 +8,9 @@ post-processing (src/tauv_vision/yolact/model/), pinned by tests/golden/gen_gold
   nms            nms.py:7-29       softmax, max over non-background, sort desc, top_k, triu IoU,
                                    column max, keep (iou_max <= thr) & (conf >= cthr); batch 0 only
   assemble_mask  masks.py:8-21     per detection sigmoid(sum_k c_k P_k) x box_to_mask (boxes.py:88-103)
+  box_encode     boxes.py:45-53    e_c = (b_c - a_c) / (v0 * a_hw) ; e_hw = log(b_hw / a_hw) / v1
+  masknet        masknet.py:8-55   protonet: [3x3 conv + LeakyReLU, ConvTranspose2d(3, s2, p1) to 2x
+                                   size + LeakyReLU] x 2, 3x3 conv + LeakyReLU, 1x1 conv + LeakyReLU
 """
 from math import sqrt
 
@@ -31,6 +34,29 @@ def box_decode(enc, anchor, variances):
     c = anchor[..., :2] + enc[..., :2] * variances[0] * anchor[..., 2:]
     hw = anchor[..., 2:] * torch.exp(enc[..., 2:] * variances[1])
     return torch.cat([c, hw], -1)
+
+
+def box_encode(box, anchor, variances):
+    c = box[..., :2] - anchor[..., :2]
+    c = c / (variances[0] * anchor[..., 2:])
+    hw = torch.log(box[..., 2:] / anchor[..., 2:]) / variances[1]
+    return torch.cat([c, hw], -1)
+
+
+def masknet(sd, x):
+    """Masknet.forward (masknet.py:44-55) over fpn[0] x [B, F, H, W] with state_dict `sd`.
+    ConvTranspose2d(3, stride 2, padding 1) called with output_size = 2x -> output_padding 1."""
+    def conv(t, name, pad):
+        return F.leaky_relu(F.conv2d(t, sd[name + ".weight"], sd[name + ".bias"], padding=pad))
+
+    def up(t, name):
+        return F.leaky_relu(F.conv_transpose2d(t, sd[name + ".weight"], sd[name + ".bias"], stride=2, padding=1,
+                                               output_padding=1))
+
+    x = up(conv(x, "_layers_1.0.0", 1), "_upsample_layer_1")
+    x = up(conv(x, "_layers_2.0.0", 1), "_upsample_layer_2")
+    x = conv(x, "_layers_3.0.0", 1)
+    return conv(x, "_output_layer", 0)
 
 
 def _corners(b):

@@ -97,6 +97,41 @@ int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cp
   });
 }
 
+// fp32 NCHW [B, C, H, W] -> NHWC compute dtype (pixel stride ldc): 64 x 64 (channel, pixel)
+// tiles transposed through LDS so both the NCHW reads and the NHWC writes are coalesced
+template <typename T>
+__global__ __launch_bounds__(256) void nchw_to_nhwc(const float* __restrict__ img, int C, int HW, int ldc,
+                                                    T* __restrict__ out) {
+  __shared__ float t[64][65];
+  const int b = blockIdx.z, c0 = blockIdx.y * 64, p0 = blockIdx.x * 64;
+  const float* src = img + (size_t)b * C * HW;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int c = i >> 6, q = i & 63;
+    t[c][q] = (c0 + c < C && p0 + q < HW) ? src[(size_t)(c0 + c) * HW + p0 + q] : 0.f;
+  }
+  __syncthreads();
+  T* dst = out + (size_t)b * HW * ldc;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int q = i >> 6, c = i & 63;
+    if (c0 + c < C && p0 + q < HW) dst[(size_t)(p0 + q) * ldc + c0 + c] = (T)t[c][q];
+  }
+}
+
+int launch_nchw_to_nhwc(const float* img, int B, int C, int H, int W, void* out, int ldc, int dtype, hipStream_t s) {
+  if (B < 1 || C < 1 || (long)H * W >= (1L << 31) || ldc < C || B > 65535) {
+    set_error("nchw_to_nhwc: bad shapes");
+    return 1;
+  }
+  const int HW = H * W;
+  dim3 grid((HW + 63) / 64, (C + 63) / 64, B);
+  return dispatch_dtype(dtype, [&](auto tag) {
+    using T = std::remove_pointer_t<decltype(tag)>;
+    hipLaunchKernelGGL(nchw_to_nhwc<T>, grid, dim3(256), 0, s, img, C, HW, ldc, (T*)out);
+    TV_HIP(hipGetLastError());
+    return 0;
+  });
+}
+
 // one thread per (target pixel, 16-byte chunk); covered rectangle [y0,y1) x [x0,x1) skipped
 __global__ void uncovered_copy(const uint4* __restrict__ add, int add_ldc16, uint4* __restrict__ out,
                                int out_ldc16, int chunks, int B, int tH, int tW, int y0, int y1, int x0, int x1) {

@@ -12,9 +12,9 @@ void set_error(const std::string& msg) { g_err = msg; }
 
 using namespace tv;
 
-#define TV_GUARD(body)                                     \
+#define TV_GUARD(...)                                      \
   try {                                                    \
-    body                                                   \
+    __VA_ARGS__                                            \
   } catch (const std::bad_alloc&) {                        \
     set_error("host allocation failed");                   \
     return TV_ENOMEM;                                      \
@@ -193,21 +193,70 @@ int tv_yolact_box_decode(const float* enc, const float* anchor, int32_t B, int32
   })
 }
 
-int tv_yolact_fast_nms(const float* cls, int32_t A, int32_t C1, const float* box, int32_t top_k, float iou_thr,
-                       float conf_thr, int64_t* det, int32_t* n_det, void* stream) {
+int tv_yolact_box_encode(const float* box, const float* anchor, int32_t B, int32_t A, int32_t anchor_batch, float v0,
+                         float v1, float* enc, void* stream) {
   TV_GUARD({
-    if (!cls || !box || !det || !n_det) { set_error("bad argument"); return TV_EINVAL; }
-    return launch_yolact_fast_nms(cls, A, C1, box, top_k, iou_thr, conf_thr, (long long*)det, n_det,
-                                  (hipStream_t)stream);
+    if (!enc || !anchor || !box) { set_error("bad argument"); return TV_EINVAL; }
+    return launch_yolact_box_encode(box, anchor, B, A, anchor_batch, v0, v1, enc, (hipStream_t)stream);
   })
 }
 
-int tv_yolact_assemble_mask(const float* proto, int32_t K, int32_t H, int32_t W, const float* coeff, const float* box,
-                            int32_t n, float* mask, void* stream) {
+int tv_yolact_nms_workspace_size(int32_t B, int32_t A, int32_t top_k, int64_t* bytes) {
+  TV_GUARD({
+    if (!bytes || B < 1 || A < 1 || top_k < 1) { set_error("bad argument"); return TV_EINVAL; }
+    const size_t n = yolact_nms_workspace_bytes(B, A, top_k);
+    if (!n) return TV_EHIP;
+    *bytes = (int64_t)n;
+    return TV_OK;
+  })
+}
+
+int tv_yolact_fast_nms_batched(const float* cls, int32_t B, int32_t A, int32_t C1, const float* box, int32_t top_k,
+                               float iou_thr, float conf_thr, int64_t* det, int32_t* n_det, void* ws, int64_t ws_bytes,
+                               void* stream) {
+  TV_GUARD({
+    if (!cls || !box || !det || !n_det || !ws || ws_bytes < 0) { set_error("bad argument"); return TV_EINVAL; }
+    const int K = top_k < A ? top_k : A;
+    return launch_yolact_fast_nms(cls, (long long)A * C1, A, C1, box, (long long)A * 4, B, top_k, iou_thr, conf_thr,
+                                  ws, (size_t)ws_bytes, (long long*)det, K, n_det, (hipStream_t)stream);
+  })
+}
+
+int tv_yolact_fast_nms(const float* cls, int32_t A, int32_t C1, const float* box, int32_t top_k, float iou_thr,
+                       float conf_thr, int64_t* det, int32_t* n_det, void* stream) {
+  TV_GUARD({
+    if (!cls || !box || !det || !n_det || A < 1 || top_k < 1) { set_error("bad argument"); return TV_EINVAL; }
+    hipStream_t s = (hipStream_t)stream;
+    const size_t need = yolact_nms_workspace_bytes(1, A, top_k);
+    if (!need) return TV_EHIP;
+    void* ws = nullptr;
+    TV_HIP(hipMallocAsync(&ws, need, s));
+    const int K = top_k < A ? top_k : A;
+    int rc = launch_yolact_fast_nms(cls, (long long)A * C1, A, C1, box, (long long)A * 4, 1, top_k, iou_thr, conf_thr,
+                                    ws, need, (long long*)det, K, n_det, s);
+    TV_HIP(hipFreeAsync(ws, s));
+    return rc;
+  })
+}
+
+int tv_yolact_assemble_mask(const float* proto, const int64_t pst[3], int32_t K, int32_t H, int32_t W,
+                            const float* coeff, const float* box, int32_t n, float* mask, void* stream) {
   TV_GUARD({
     if (n == 0) return TV_OK;
-    if (!proto || !coeff || !mask) { set_error("bad argument"); return TV_EINVAL; }
-    return launch_yolact_assemble_mask(proto, K, H, W, coeff, box, n, mask, (hipStream_t)stream);
+    if (!proto || !pst || !coeff || !mask || n < 0) { set_error("bad argument"); return TV_EINVAL; }
+    const long long st[4] = {0, pst[0], pst[1], pst[2]};
+    return launch_yolact_assemble_mask(proto, st, 1, K, H, W, coeff, box, nullptr, n, mask, (hipStream_t)stream);
+  })
+}
+
+int tv_yolact_assemble_masks(const float* proto, const int64_t pst[4], int32_t B, int32_t K, int32_t H, int32_t W,
+                             const float* coeff, const float* box, const int32_t* counts, int32_t n_max, float* mask,
+                             void* stream) {
+  TV_GUARD({
+    if (n_max == 0) return TV_OK;
+    if (!proto || !pst || !coeff || !mask || n_max < 0) { set_error("bad argument"); return TV_EINVAL; }
+    const long long st[4] = {pst[0], pst[1], pst[2], pst[3]};
+    return launch_yolact_assemble_mask(proto, st, B, K, H, W, coeff, box, counts, n_max, mask, (hipStream_t)stream);
   })
 }
 

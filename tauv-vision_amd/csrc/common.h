@@ -146,6 +146,8 @@ int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad,
                      hipStream_t s);
 int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cpad, int dtype,
                    hipStream_t s);
+// fp32 NCHW [B, C, H, W] -> NHWC compute dtype with pixel stride ldc (protonet input)
+int launch_nchw_to_nhwc(const float* img, int B, int C, int H, int W, void* out, int ldc, int dtype, hipStream_t s);
 // out[target] = add[target] for target pixels not covered by the shifted upsample.
 // CenterpointDLA34 bandwidth kernels (dla34.hip): NHWC, channels in whole 16-byte chunks.
 // MaxPool2d(2, 2, ceil_mode=True): out [B, ceil(H/2), ceil(W/2), C]
@@ -157,14 +159,21 @@ int launch_dcn_sample(const void* x, int B, int H, int W, int C, const void* om,
 // (sy, sx) = pad_to_match's (pad_above, pad_left)
 int launch_dwconvt_add(const void* src, int B, int h, int w, int C, const float* weight, int f, const void* add,
                        int add_ldc, void* out, int tH, int tW, int sy, int sx, int dtype, hipStream_t s);
-// YOLACT post-processing (yolact.hip), fp32: box_decode (boxes.py:55-61), batch-0 fast NMS
-// (nms.py:7-29; det = kept anchor indices in descending-confidence order), assemble_mask (masks.py:8-21)
+// YOLACT post-processing (yolact.hip), fp32: box_decode (boxes.py:55-61), box_encode (:45-53),
+// fast NMS of B images (nms.py:7-29; det[b] = kept anchor indices in descending-confidence order,
+// n_det[b] their number), assemble_mask over B images (masks.py:8-21; prototypes at element strides
+// pst = (batch, k, y, x), coefficients [B][n_max][K], boxes [B][n_max][4] or null, counts [B] or null)
 int launch_yolact_box_decode(const float* enc, const float* anchor, int B, int A, int anchor_batch, float v0, float v1,
                              float* out, hipStream_t s);
-int launch_yolact_fast_nms(const float* cls, int A, int C1, const float* box, int top_k, float iou_thr, float conf_thr,
-                           long long* det, int* n_det, hipStream_t s);
-int launch_yolact_assemble_mask(const float* proto, int K, int H, int W, const float* coeff, const float* box, int n,
-                                float* out, hipStream_t s);
+int launch_yolact_box_encode(const float* box, const float* anchor, int B, int A, int anchor_batch, float v0, float v1,
+                             float* out, hipStream_t s);
+size_t yolact_nms_workspace_bytes(int B, int A, int top_k);
+int launch_yolact_fast_nms(const float* cls, long long cls_bstride, int A, int C1, const float* box,
+                           long long box_bstride, int B, int top_k, float iou_thr, float conf_thr, void* ws,
+                           size_t ws_bytes, long long* det, int det_stride, int* n_det, hipStream_t s);
+int launch_yolact_assemble_mask(const float* proto, const long long pst[4], int B, int K, int H, int W,
+                                const float* coeff, const float* box, const int* counts, int n_max, float* out,
+                                hipStream_t s);
 int launch_uncovered_copy(const void* add, int add_ldc, void* out, int out_ldc, int C, int B,
                           int tH, int tW, int y0, int y1, int x0, int x1, int dtype,
                           hipStream_t s);

@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_igemm(const ConvParams* __re
       const size_t tpix = (size_t)(b * p.tH + Y) * p.tW + X;
       const T* ad = reinterpret_cast<const T*>(p.add) + tpix * p.add_ldc + co;
       float v[OVEC];
-      const uint4 raw = gload16(ad);
+      const uint4 raw = p.add ? gload16(ad) : make_uint4(0, 0, 0, 0);  // no skip tensor: plain scatter
       const uint32_t rw4[4] = {raw.x, raw.y, raw.z, raw.w};
       if constexpr (sizeof(T) == 4) {
 #pragma unroll

@@ -303,7 +303,8 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
       const int X = ox * p.up_s + pj + p.sx;
       const bool ok = n < p.N && m < p.M && Y < p.tH && X < p.tW;
       toff[k] = ok ? (size_t)(b * p.tH + Y) * p.tW + X : ~(size_t)0;
-      av[k] = ok ? gload16(reinterpret_cast<const T*>(p.add) + toff[k] * p.add_ldc + co) : make_uint4(0, 0, 0, 0);
+      av[k] = ok && p.add ? gload16(reinterpret_cast<const T*>(p.add) + toff[k] * p.add_ldc + co)
+                          : make_uint4(0, 0, 0, 0);  // no skip tensor (protonet ConvT phases): plain scatter
     }
 #pragma unroll
     for (int k = 0; k < NP; ++k) {

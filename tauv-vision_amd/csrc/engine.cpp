@@ -85,7 +85,7 @@ int Engine::pack_op(size_t oi) {
   Packed& pk = packed[oi];
   const int esz = dtype_size(dtype);
   const int BK = 128 / esz;
-  if (op.kind == OP_PREP || op.kind == OP_MAXPOOL || op.kind == OP_DCN) return TV_OK;
+  if (op.kind == OP_PREP || op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_LAYOUT_IN) return TV_OK;
   if (op.kind == OP_DWCONVT_ADD) {  // depthwise ConvTranspose2d weight [C][1][2f][2f] -> fp32 [2f][2f][C]
     const int c = op.N, k = 2 * op.up_s;
     const float* w = weight(op.up_w + ".weight", (int64_t)c * k * k);
@@ -122,6 +122,9 @@ int Engine::pack_op(size_t oi) {
         }
   } else {
     const int N = op.N;
+    // rows of the PyTorch weight: a plain conv into the caller's fp32 output stores out_cpad
+    // columns of an out_c-channel conv (protonet _output_layer)
+    const int wN = (op.out < 0 && op.stack_w.empty()) ? plan.out_c : N;
     pk.Npad = (int)align_up(N, kTile);
     int kbase = 0;
     pk.seg_ksteps.clear();
@@ -175,14 +178,38 @@ int Engine::pack_op(size_t oi) {
           if (o.wname == sg.wname) wcin = std::max(wcin, o.ci0 + o.cin);
         const int re = sg.row_expand;  // row-expanded input: K index = ky * cs + kx * cin + c
         const int kk = re ? sg.kh * re : sg.kh * sg.kw;
-        const float* w = weight(sg.wname + ".weight", (int64_t)N * wcin * kk);
+        if (sg.convt_phase >= 0) {
+          // ConvTranspose2d(3, s2, p1) weight [cin][cout][3][3], one output parity (pi, pj): tap
+          // (dy, dx) of the phase conv reads input (m + dy, n + dx) and uses kernel element
+          // ky = 1 (pi = 0) or 2 - 2 dy (pi = 1) — out[2m + pi] += x[m + dy] W[ky] with
+          // 2m + pi = 2(m + dy) - 1 + ky — and kx likewise
+          const float* w = weight(sg.wname + ".weight", (int64_t)wcin * wN * 9);
+          if (!w) return TV_ENOTFOUND;
+          std::vector<double> scale, shift;
+          int rc = fold(sg.wname, "", wN, scale, shift);
+          if (rc) return rc;
+          for (int co = 0; co < wN; ++co) bias[co] += (float)shift[co];
+          const int pi = sg.convt_phase >> 1, pj = sg.convt_phase & 1;
+          for (int dy = 0; dy < sg.kh; ++dy)
+            for (int dx = 0; dx < sg.kw; ++dx) {
+              const int ky = pi == 0 ? 1 : 2 - 2 * dy, kx = pj == 0 ? 1 : 2 - 2 * dx;
+              const int t = dy * sg.kw + dx;
+              for (int co = 0; co < wN; ++co)
+                for (int ci = 0; ci < sg.cin; ++ci)
+                  hw[(size_t)co * pk.Kpad + (size_t)kb * BK + (size_t)t * cs + ci] =
+                      w[(((size_t)(sg.ci0 + ci) * wN + co) * 3 + ky) * 3 + kx];
+            }
+          kb += pk.seg_ksteps[si];
+          continue;
+        }
+        const float* w = weight(sg.wname + ".weight", (int64_t)wN * wcin * kk);
         if (!w) return TV_ENOTFOUND;
         std::vector<double> scale, shift;
-        int rc = fold(sg.wname, sg.bn, N, scale, shift);
+        int rc = fold(sg.wname, sg.bn, wN, scale, shift);
         if (rc) return rc;
         if (seen.insert(sg.wname).second)
-          for (int co = 0; co < N; ++co) bias[co] += (float)shift[co];
-        for (int co = 0; co < N; ++co)
+          for (int co = 0; co < wN; ++co) bias[co] += (float)shift[co];
+        for (int co = 0; co < wN; ++co)
           for (int ci = 0; ci < sg.cin; ++ci)
             for (int t = 0; t < kk; ++t) {
               const size_t k = re ? (size_t)(t / re) * cs + (t % re) * sg.cin + ci : (size_t)t * cs + ci;
@@ -341,11 +368,14 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->off.assign(nt, 0);
   struct Live { size_t off, size; int last; };
   std::vector<Live> live;
+  std::vector<char> placed(nt, 0);  // a tensor written by several ops (ConvT phases) is placed once
   size_t peak = 0;
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     live.erase(std::remove_if(live.begin(), live.end(), [&](const Live& l) { return l.last < (int)i; }), live.end());
     if (op.out < 0 || (stem_op >= 0 && op.kind == OP_PREP)) continue;  // fused stem: no staged input
+    if (placed[op.out]) continue;
+    placed[op.out] = 1;
     const TensorSpec& t = plan.tensors[op.out];
     size_t sz = align_up((size_t)B * t.H * t.W * t.C * esz, 256);
     std::sort(live.begin(), live.end(), [](const Live& a, const Live& b) { return a.off < b.off; });
@@ -385,8 +415,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
                                sg.pad_w >= 0 ? sg.pad_w : sg.pad, pk.seg_ksteps[s], kbase};
         kbase += pk.seg_ksteps[s];
       }
-      const int Ho = op.out >= 0 ? plan.tensors[op.out].H : plan.out_h;
-      const int Wo = op.out >= 0 ? plan.tensors[op.out].W : plan.out_w;
+      const int Ho = op.up_s ? op.gh : op.out >= 0 ? plan.tensors[op.out].H : plan.out_h;
+      const int Wo = op.up_s ? op.gw : op.out >= 0 ? plan.tensors[op.out].W : plan.out_w;
       p.Ho = Ho;
       p.Wo = Wo;
       p.M = B * Ho * Wo;
@@ -396,6 +426,17 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.out_coff = 0;
       p.mtiles = (p.M + kTile - 1) / kTile;
       p.ntiles = pk.Npad / kTile;
+      if (op.up_s) {  // phase scatter into the high-resolution output (protonet ConvT phases)
+        const TensorSpec& tgt = plan.tensors[op.out];
+        p.up_s = op.up_s;
+        p.up_cout = op.N;
+        p.tH = tgt.H;
+        p.tW = tgt.W;
+        p.sy = op.sy;
+        p.sx = op.sx;
+        p.add = op.add >= 0 ? base + ws->off[op.add] : nullptr;
+        p.add_ldc = op.add >= 0 ? plan.tensors[op.add].C : 0;
+      }
     } else {
       const TensorSpec& src = plan.tensors[op.src];
       const TensorSpec& tgt = plan.tensors[op.out];
@@ -650,6 +691,14 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     sp.bias = packed[i].bias;
     return launch_stem(sp, dtype, cu_count, s);
   }
+  if (op.kind == OP_LAYOUT_IN) {
+    if (input_u8) {
+      set_error("this model takes an fp32 NCHW feature map, not u8 frames");
+      return TV_EINVAL;
+    }
+    return launch_nchw_to_nhwc((const float*)input, ws->B, op.N, desc.in_h, desc.in_w, base + ws->off[op.out],
+                               plan.tensors[op.out].C, dtype, s);
+  }
   if (op.kind == OP_PREP) {
     void* dst = base + ws->off[op.out];
     return input_u8 ? launch_prep_u8((const uint8_t*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s)
@@ -685,7 +734,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   ConvParams p = ws->params[i];
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
-  const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
+  const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
                                            ws->c3_res[i], ws->c3_ni[i])
@@ -775,7 +824,8 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
     SideStreams* ss = nullptr;
     int rc = get_side(s, (int)sz.size() - 1, &ss);
     if (rc) return rc;
-    const size_t in_frame = input_u8 ? (size_t)desc.in_h * desc.in_w * 3 : (size_t)3 * desc.in_h * desc.in_w * 4;
+    const size_t in_frame = input_u8 ? (size_t)desc.in_h * desc.in_w * 3
+                                     : (size_t)plan.in_channels * desc.in_h * desc.in_w * 4;
     const size_t out_frame = (size_t)plan.out_h * plan.out_w * plan.out_cpad;
     TV_HIP(hipEventRecord(ss->fork, s));
     size_t f0 = (size_t)sz[0];
@@ -810,7 +860,8 @@ const char* Engine::op_kernel(int B, size_t i) {
                                      {"tv::stem::stem_conv<__bf16, false>", "tv::stem::stem_conv<__bf16, true>"}};
       return sn[dtype == BF16][profiled_u8 ? 1 : 0];
     }
-    const int mode = op.kind == OP_CONVT_ADD ? 1 : 0;
+    if (op.kind == OP_LAYOUT_IN) return dtype == F32 ? "tv::nchw_to_nhwc<float>" : dtype == F16 ? "tv::nchw_to_nhwc<_Float16>" : "tv::nchw_to_nhwc<__bf16>";
+    const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;
     const char* t = tn[dtype];
     const char* o = (op.out < 0) ? "float" : t;
     std::string& name = ws->kname[i];

@@ -301,6 +301,7 @@ struct Walker {
 
 int build_plan(const tv_model_desc& d, Plan* plan) {
   if (d.arch == TV_ARCH_DLA34) return build_plan_dla34(d, plan);
+  if (d.arch == TV_ARCH_PROTONET) return build_plan_protonet(d, plan);
   if (d.arch != TV_ARCH_CENTERNET) {
     set_error("unknown model arch");
     return TV_EINVAL;

@@ -28,6 +28,11 @@ struct SegSpec {
   int row_expand = 0;    // k > 0: `src` holds the k horizontal taps of a k x k conv per pixel
                          // (DCN columns: k = 9 taps of a 3x3 weight per pixel, kh = kw = 1)
   bool identity = false; // residual added as-is (BasicBlock residual = x): an identity 1x1 weight
+  // >= 0: one output phase (pi * 2 + pj) of a ConvTranspose2d(3, stride 2, padding 1) weight
+  // [cin][cout][3][3] (masknet.py:21,33): the phase's taps as a kh x kw (= 1 + pi, 1 + pj) conv
+  // with no padding over the low-resolution input (tap dy reads row oy + dy: ky = 1 for pi = 0,
+  // ky = 2 - 2 dy for pi = 1; the same along x)
+  int convt_phase = -1;
 };
 
 enum OpKind {
@@ -38,8 +43,9 @@ enum OpKind {
   OP_MAXPOOL = 3,    // MaxPool2d(2, 2, ceil_mode=True) of `src` (Tree.downsample, :199-200)
   OP_DCN = 4,        // DCNv2 sampling: columns [9 taps][C] per pixel of `src` at the offsets /
                      // sigmoid(mask logits) in tensor `add` (18 offsets, 9 logits; :386-392)
-  OP_DWCONVT_ADD = 5 // depthwise ConvTranspose2d(2f, f, f//2) of `src` + pad_to_match + `add`
-                     // (IDAUp, :446-451); up_s = f, (sy, sx) = (pad_above, pad_left)
+  OP_DWCONVT_ADD = 5, // depthwise ConvTranspose2d(2f, f, f//2) of `src` + pad_to_match + `add`
+                      // (IDAUp, :446-451); up_s = f, (sy, sx) = (pad_above, pad_left)
+  OP_LAYOUT_IN = 6    // fp32 NCHW input with N channels -> NHWC compute dtype (protonet fpn[0] input)
 };
 
 struct OpSpec {
@@ -60,6 +66,9 @@ struct OpSpec {
   std::string up_w;           // ConvTranspose2d prefix
   int cov_y0 = 0, cov_y1 = 0, cov_x0 = 0, cov_x1 = 0;  // covered target rectangle
   double flops = 0;           // algorithmic FLOPs per frame (2*MAC)
+  // OP_CONV with up_s > 0: a phase-scatter GEMM over the (gh, gw) grid of its input whose output
+  // pixel (oy, ox) lands at (oy * up_s + sy, ox * up_s + sx) of `out` (no skip tensor when add < 0)
+  int gh = 0, gw = 0;
 };
 
 struct TensorSpec {
@@ -72,6 +81,7 @@ struct Plan {
   std::vector<OpSpec> ops;
   int out_h = 0, out_w = 0, out_c = 0, out_cpad = 0;
   int in_cpad = 0;
+  int in_channels = 3;               // channels of one input frame (fp32 NCHW path)
   double flops_per_frame = 0;
   std::set<std::string> names;       // every key of `params`
 };
@@ -79,5 +89,6 @@ struct Plan {
 // Returns 0 or a TV_E* code (with tv_last_error set).
 int build_plan(const tv_model_desc& d, Plan* plan);
 int build_plan_dla34(const tv_model_desc& d, Plan* plan);  // planner_dla34.cpp
+int build_plan_protonet(const tv_model_desc& d, Plan* plan);  // planner_protonet.cpp
 
 }  // namespace tv

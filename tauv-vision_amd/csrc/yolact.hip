@@ -1,13 +1,30 @@
 // YOLACT post-processing on gfx950 (reference src/tauv_vision/yolact/model/):
 //   box_decode     boxes.py:55-61   c = a_c + e_c * v0 * a_hw, hw = a_hw * exp(e_hw * v1)
+//   box_encode     boxes.py:45-53   e_c = (b_c - a_c) / (v0 * a_hw), e_hw = log(b_hw / a_hw) / v1
 //   fast_nms       nms.py:7-29      softmax -> max non-background confidence -> descending sort ->
 //                                   top_k -> upper-triangular IoU (boxes.py:64-85) -> column max ->
-//                                   keep (iou_max <= thr) & (conf >= cthr); batch 0 only (:14, 25)
+//                                   keep (iou_max <= thr) & (conf >= cthr)
 //   assemble_mask  masks.py:8-21    sigmoid(sum_k c_k P_k) x inclusive box mask (boxes.py:88-103)
 // All fp32 (the reference runs them in fp32), expression order as in the reference.
-// fast_nms is one workgroup: the whole problem (<= 16384 anchors, top_k <= 1024) lives in LDS —
-// a bitonic sort of (confidence, anchor) keys, then one thread per kept column j scans i < j.
+//
+// fast_nms, any anchor count, B images per launch (the reference runs image 0 only: :14,25):
+//   nms_keys    one thread per anchor: the confidence as an order-preserving 32-bit key;
+//   sort        rocPRIM segmented radix sort (one segment per image, descending, stable: equal
+//               confidences keep ascending anchor order), values = anchor ids;
+//   nms_iou     one thread per kept column j < min(top_k, A); rows i < j staged through LDS in
+//               256-box chunks; the column max propagates NaN like torch.max (0/0 IoUs of two
+//               zero-area boxes drop the column: NaN <= thr is false);
+//   nms_compact one workgroup per image: order-preserving compaction of the kept columns.
+// assemble_mask: one workgroup per 1024 pixels of one image; the block's prototypes (any
+// strides: NCHW or the protonet's NHWC output) are staged in LDS as [k][pixel], each thread
+// forms 4 adjacent pixels of every detection and stores them as one 16-byte vector (the kernel
+// is HBM-write-bound: n x H x W x 4 bytes per image).
 #include "common.h"
+
+#include <cstring>
+#include <mutex>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 // the reference rounds every product before the sum (separate torch ops): no FMA contraction
 #pragma clang fp contract(off)
@@ -32,104 +49,212 @@ __global__ __launch_bounds__(256) void box_decode(const float* __restrict__ enc,
   reinterpret_cast<float4*>(out)[i] = o;
 }
 
-constexpr int kNmsThreads = 1024;
-constexpr int kNmsMaxAnchors = 16384;
-
-// keys: confidence bits (non-negative floats order like their bit patterns) in the high word,
-// ~anchor in the low word, so the descending sort breaks exact ties toward the smaller anchor
-__global__ __launch_bounds__(kNmsThreads) void fast_nms(const float* __restrict__ cls, int A, int C1,
-                                                        const float* __restrict__ box, int top_k, float iou_thr,
-                                                        float conf_thr, long long* __restrict__ det,
-                                                        int* __restrict__ n_det) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long keys[];  // [P] (P = pow2 >= A)
-  const int tid = threadIdx.x;
-  int P = 1;
-  while (P < A) P <<= 1;
-  for (int a = tid; a < P; a += kNmsThreads) {
-    unsigned long long key = 0;  // padding sorts last
-    if (a < A) {
-      const float* c = cls + (size_t)a * C1;
-      float m = c[0];
-      for (int j = 1; j < C1; ++j) m = fmaxf(m, c[j]);
-      float s = 0.f;
-      for (int j = 0; j < C1; ++j) s += expf(c[j] - m);
-      float best = 0.f;
-      for (int j = 1; j < C1; ++j) best = fmaxf(best, expf(c[j] - m) / s);
-      key = ((unsigned long long)__float_as_uint(best) << 32) | (unsigned)(~(unsigned)a);
-    }
-    keys[a] = key;
-  }
-  __syncthreads();
-  // bitonic sort, descending
-  for (int k = 2; k <= P; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < P; i += kNmsThreads) {
-        const int l = i ^ j;
-        if (l > i) {
-          const unsigned long long a = keys[i], b = keys[l];
-          const bool desc = (i & k) == 0;
-          if (desc ? a < b : a > b) {
-            keys[i] = b;
-            keys[l] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  const int K = min(top_k, A);
-  // column j survives if no higher-confidence box i < j overlaps it by more than iou_thr
-  for (int j = tid; j < K; j += kNmsThreads) {
-    const unsigned aj = ~(unsigned)(keys[j] & 0xffffffffu);
-    const float conf = __uint_as_float((unsigned)(keys[j] >> 32));
-    const float4 bj = reinterpret_cast<const float4*>(box)[aj];
-    // corners (boxes.py:14-26) and area (:79-80) exactly as the reference forms them
-    const float jy0 = bj.x - bj.z / 2, jx0 = bj.y - bj.w / 2, jy1 = bj.x + bj.z / 2, jx1 = bj.y + bj.w / 2;
-    const float area_j = bj.z * bj.w;
-    float iou_max = 0.f;  // torch.triu zeroes i >= j; the max includes those zeros
-    for (int i = 0; i < j; ++i) {
-      const unsigned ai = ~(unsigned)(keys[i] & 0xffffffffu);
-      const float4 bi = reinterpret_cast<const float4*>(box)[ai];
-      const float iy0 = bi.x - bi.z / 2, ix0 = bi.y - bi.w / 2, iy1 = bi.x + bi.z / 2, ix1 = bi.y + bi.w / 2;
-      const float ih = fmaxf(fminf(iy1, jy1) - fmaxf(iy0, jy0), 0.f);
-      const float iw = fmaxf(fminf(ix1, jx1) - fmaxf(ix0, jx0), 0.f);
-      const float inter = ih * iw;
-      const float uni = (bi.z * bi.w + area_j) - inter;
-      iou_max = fmaxf(iou_max, inter / uni);
-    }
-    const bool keep = iou_max <= iou_thr && conf >= conf_thr;
-    // order-preserving compaction: write a flag, compact after the barrier
-    reinterpret_cast<int*>(keys + P)[j] = keep ? 1 : 0;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int n = 0;
-    const int* flag = reinterpret_cast<const int*>(keys + P);
-    for (int j = 0; j < K; ++j)
-      if (flag[j]) det[n++] = (long long)(~(unsigned)(keys[j] & 0xffffffffu));
-    *n_det = n;
-  }
+__global__ __launch_bounds__(256) void box_encode(const float* __restrict__ box, const float* __restrict__ anchor,
+                                                  int B, int A, int anchor_batch, float v0, float v1,
+                                                  float* __restrict__ out) {
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (unsigned)B * A) return;
+  const unsigned b = i / (unsigned)A, a = i % (unsigned)A;
+  const float4 g = reinterpret_cast<const float4*>(box)[i];
+  const float4 an = reinterpret_cast<const float4*>(anchor)[(anchor_batch == 1 ? 0 : b) * (unsigned)A + a];
+  float4 o;
+  // g_cxcy = box[:2] - anchor[:2]; g_cxcy /= (v0 * anchor[2:]); g_wh = log(box[2:] / anchor[2:]) / v1
+  o.x = (g.x - an.x) / (v0 * an.z);
+  o.y = (g.y - an.y) / (v0 * an.w);
+  o.z = logf(g.z / an.z) / v1;
+  o.w = logf(g.w / an.w) / v1;
+  reinterpret_cast<float4*>(out)[i] = o;
 }
 
-// out[n][y][x] = sigmoid(sum_k coeff[n][k] * proto[k][y][x]) * box_mask(n, y, x)
-__global__ __launch_bounds__(256) void assemble_mask(const float* __restrict__ proto, int K, int H, int W,
-                                                     const float* __restrict__ coeff, const float* __restrict__ box,
-                                                     int n, float* __restrict__ out) {
+__device__ __forceinline__ uint32_t order_bits(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float unorder_bits(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+
+// max over classes 1.. of softmax(cls row) (nms.py:10-11)
+__global__ __launch_bounds__(256) void nms_keys(const float* __restrict__ cls, long long cls_bstride, int A, int C1,
+                                                int B, uint32_t* __restrict__ keys) {
   const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
-  const unsigned hw = (unsigned)H * W;
-  if (i >= (unsigned)n * hw) return;
-  const unsigned d = i / hw, pix = i % hw;
-  const unsigned y = pix / (unsigned)W, x = pix % (unsigned)W;
+  if (i >= (unsigned)B * A) return;
+  const unsigned b = i / (unsigned)A, a = i % (unsigned)A;
+  const float* c = cls + (size_t)b * cls_bstride + (size_t)a * C1;
+  float m = c[0];
+  for (int j = 1; j < C1; ++j) m = fmaxf(m, c[j]);
   float s = 0.f;
-  for (int k = 0; k < K; ++k) s += coeff[(size_t)d * K + k] * proto[(size_t)k * hw + pix];
-  float m = 1.f / (1.f + expf(-s));
-  if (box) {
-    const float* b = box + (size_t)d * 4;
-    const float by = b[0] * (float)H, bx = b[1] * (float)W, bh = b[2] * (float)H, bw = b[3] * (float)W;
-    const float left = bx - bw / 2, right = bx + bw / 2, top = by - bh / 2, bottom = by + bh / 2;
-    const float fx = (float)x, fy = (float)y;
-    m *= (fx >= left && fx <= right && fy >= top && fy <= bottom) ? 1.f : 0.f;
+  for (int j = 0; j < C1; ++j) s += expf(c[j] - m);
+  float best = 0.f;
+  for (int j = 1; j < C1; ++j) best = fmaxf(best, expf(c[j] - m) / s);
+  keys[i] = order_bits(best);
+}
+
+constexpr int kIouThreads = 256;
+
+// keep[b][j] for the K highest-confidence anchors of image b (sorted order)
+__global__ __launch_bounds__(kIouThreads) void nms_iou(const float* __restrict__ box, long long box_bstride, int A,
+                                                       int K, const uint32_t* __restrict__ skeys,
+                                                       const int* __restrict__ sidx, float iou_thr, float conf_thr,
+                                                       uint8_t* __restrict__ keep) {
+  __shared__ float4 corner[kIouThreads];  // y0, x0, y1, x1 of the staged rows
+  __shared__ float area[kIouThreads];
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * kIouThreads + threadIdx.x;
+  const size_t seg = (size_t)b * A;
+  const float4* bx = reinterpret_cast<const float4*>(box + (size_t)b * box_bstride);
+  float jy0 = 0, jx0 = 0, jy1 = 0, jx1 = 0, area_j = 0, conf = 0;
+  if (j < K) {
+    const float4 bj = bx[sidx[seg + j] - (int)seg];
+    // corners (boxes.py:14-26) and area (:79-80) exactly as the reference forms them
+    jy0 = bj.x - bj.z / 2; jx0 = bj.y - bj.w / 2; jy1 = bj.x + bj.z / 2; jx1 = bj.y + bj.w / 2;
+    area_j = bj.z * bj.w;
+    conf = unorder_bits(skeys[seg + j]);
   }
-  out[i] = m;
+  float iou_max = 0.f;  // torch.triu zeroes i >= j; the max includes those zeros
+  const int jmax = min(K, (int)(blockIdx.x + 1) * kIouThreads);  // rows needed by this block: i < jmax - 1
+  for (int i0 = 0; i0 < jmax - 1; i0 += kIouThreads) {
+    __syncthreads();
+    const int ii = i0 + threadIdx.x;
+    if (ii < K) {
+      const float4 bi = bx[sidx[seg + ii] - (int)seg];
+      corner[threadIdx.x] = make_float4(bi.x - bi.z / 2, bi.y - bi.w / 2, bi.x + bi.z / 2, bi.y + bi.w / 2);
+      area[threadIdx.x] = bi.z * bi.w;
+    }
+    __syncthreads();
+    const int n = min(kIouThreads, j - i0);  // rows i0 .. j-1 of this chunk
+    for (int t = 0; t < n; ++t) {
+      const float4 ci = corner[t];
+      const float ih = fmaxf(fminf(ci.z, jy1) - fmaxf(ci.x, jy0), 0.f);
+      const float iw = fmaxf(fminf(ci.w, jx1) - fmaxf(ci.y, jx0), 0.f);
+      const float inter = ih * iw;
+      const float v = inter / ((area[t] + area_j) - inter);
+      iou_max = (v > iou_max || v != v) ? v : iou_max;  // NaN sticks (torch.max propagates it)
+    }
+  }
+  if (j < K) keep[(size_t)b * K + j] = (iou_max <= iou_thr && conf >= conf_thr) ? 1 : 0;
+}
+
+constexpr int kCompactThreads = 1024;
+
+__global__ __launch_bounds__(kCompactThreads) void nms_compact(const uint8_t* __restrict__ keep, int A, int K,
+                                                               const int* __restrict__ sidx, long long* __restrict__ det,
+                                                               int det_stride, int* __restrict__ n_det) {
+  __shared__ int wsum[kCompactThreads / 64];
+  __shared__ int base;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) base = 0;
+  for (int j0 = 0; j0 < K; j0 += kCompactThreads) {
+    const int j = j0 + tid;
+    const int f = j < K ? keep[(size_t)b * K + j] : 0;
+    const unsigned long long m = __ballot(f);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();  // `base` of the previous chunk is final
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    if (f) det[(size_t)b * det_stride + off + before] = (long long)(sidx[(size_t)b * A + j] - b * A);
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int w = 0; w < kCompactThreads / 64; ++w) t += wsum[w];
+      base += t;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) n_det[b] = base;
+}
+
+__global__ void segment_offsets(int* off, int B, int A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i <= B) off[i] = i * A;
+}
+
+// masks[b][d][y][x] = sigmoid(sum_k coeff[b][d][k] * proto[b][k][y][x]) * box_mask(b, d, y, x)
+constexpr int kMaskThreads = 256;
+constexpr int kMaskPix = 4 * kMaskThreads;  // pixels per workgroup (4 adjacent per thread)
+
+struct MaskParams {
+  const float* proto;
+  long long ps_b, ps_k, ps_y, ps_x;  // element strides
+  int K, H, W;
+  const float* coeff;                // [B][n_max][K]
+  const float* box;                  // [B][n_max][4] or null
+  const int* counts;                 // [B] or null (= n_max)
+  int n_max;
+  float* out;                        // [B][n_max][H][W]
+};
+
+__global__ __launch_bounds__(kMaskThreads) void assemble_mask(const MaskParams p) {
+  extern __shared__ __attribute__((aligned(16))) float pr[];  // [K][kMaskPix]
+  const int b = blockIdx.y;
+  const int n = p.counts ? min(p.counts[b], p.n_max) : p.n_max;
+  if (n <= 0) return;
+  const int hw = p.H * p.W;
+  const int pix0 = blockIdx.x * kMaskPix;
+  const float* pb = p.proto + (size_t)b * p.ps_b;
+  // stage the block's prototypes: element (k, q) at pr[k * kMaskPix + q]; consecutive threads
+  // walk the stride-1 axis (channels for NHWC views, pixels for NCHW)
+  const bool chan_fast = p.ps_k < p.ps_x;
+  for (int e = threadIdx.x; e < p.K * kMaskPix; e += kMaskThreads) {
+    int k, q;
+    if (chan_fast) { k = e % p.K; q = e / p.K; } else { q = e % kMaskPix; k = e / kMaskPix; }
+    const int pix = pix0 + q;
+    float v = 0.f;
+    if (pix < hw) {
+      const int y = pix / p.W, x = pix - y * p.W;
+      v = pb[(size_t)k * p.ps_k + (size_t)y * p.ps_y + (size_t)x * p.ps_x];
+    }
+    pr[k * kMaskPix + q] = v;
+  }
+  __syncthreads();
+  const int q0 = 4 * threadIdx.x;
+  const int pix = pix0 + q0;
+  if (pix >= hw) return;
+  int yy[4], xx[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    yy[e] = (pix + e) / p.W;
+    xx[e] = (pix + e) - yy[e] * p.W;
+  }
+  const bool vec = (hw & 3) == 0;  // 16-byte stores: every row of a detection starts 16-byte aligned
+  const float* cb = p.coeff + (size_t)b * p.n_max * p.K;
+  const float* bb = p.box ? p.box + (size_t)b * p.n_max * 4 : nullptr;
+  float* ob = p.out + (size_t)b * p.n_max * hw;
+  for (int d = 0; d < n; ++d) {
+    const float* c = cb + (size_t)d * p.K;
+    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < p.K; ++k) {
+      const float ck = c[k];
+      const float4 v = *reinterpret_cast<const float4*>(pr + k * kMaskPix + q0);
+      s[0] += ck * v.x;
+      s[1] += ck * v.y;
+      s[2] += ck * v.z;
+      s[3] += ck * v.w;
+    }
+    float m[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m[e] = 1.f / (1.f + expf(-s[e]));
+    if (bb) {
+      const float* q = bb + (size_t)d * 4;
+      const float by = q[0] * (float)p.H, bx = q[1] * (float)p.W, bh = q[2] * (float)p.H, bw = q[3] * (float)p.W;
+      const float left = bx - bw / 2, right = bx + bw / 2, top = by - bh / 2, bottom = by + bh / 2;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float fx = (float)xx[e], fy = (float)yy[e];
+        m[e] *= (fx >= left && fx <= right && fy >= top && fy <= bottom) ? 1.f : 0.f;
+      }
+    }
+    float* o = ob + (size_t)d * hw + pix;
+    if (vec) {
+      *reinterpret_cast<float4*>(o) = make_float4(m[0], m[1], m[2], m[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (pix + e < hw) o[e] = m[e];
+    }
+  }
 }
 
 }  // namespace yolact
@@ -147,36 +272,114 @@ int launch_yolact_box_decode(const float* enc, const float* anchor, int B, int A
   return 0;
 }
 
-int launch_yolact_fast_nms(const float* cls, int A, int C1, const float* box, int top_k, float iou_thr, float conf_thr,
-                           long long* det, int* n_det, hipStream_t s) {
-  if (A < 1 || A > yolact::kNmsMaxAnchors / 2 || C1 < 2 || top_k < 1) {
-    set_error("fast_nms: need 1 <= anchors <= 8192, >= 2 classes (incl. background), top_k >= 1");
-    return 2;  // TV_ESHAPE
+int launch_yolact_box_encode(const float* box, const float* anchor, int B, int A, int anchor_batch, float v0, float v1,
+                             float* out, hipStream_t s) {
+  if (B < 1 || A < 1 || (anchor_batch != 1 && anchor_batch != B) || (long)B * A >= (1L << 31)) {
+    set_error("box_encode: bad shapes (anchor batch must be 1 or B)");
+    return 2;
   }
-  int P = 1;
-  while (P < A) P <<= 1;
-  const size_t lds = (size_t)P * 8 + (size_t)std::min(top_k, A) * 4 + 16;
-  static bool attr = false;
-  if (!attr) {
-    TV_HIP(hipFuncSetAttribute((const void*)yolact::fast_nms, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
-  }
-  hipLaunchKernelGGL(yolact::fast_nms, dim3(1), dim3(yolact::kNmsThreads), lds, s, cls, A, C1, box, top_k, iou_thr,
-                     conf_thr, det, n_det);
+  const unsigned n = (unsigned)B * A;
+  hipLaunchKernelGGL(yolact::box_encode, dim3((n + 255) / 256), dim3(256), 0, s, box, anchor, B, A, anchor_batch, v0,
+                     v1, out);
   TV_HIP(hipGetLastError());
   return 0;
 }
 
-int launch_yolact_assemble_mask(const float* proto, int K, int H, int W, const float* coeff, const float* box, int n,
-                                float* out, hipStream_t s) {
-  if (K < 1 || H < 1 || W < 1 || n < 0 || (long)n * H * W >= (1L << 31)) {
+namespace {
+
+struct NmsLayout {
+  size_t keys, skeys, sidx, keep, offs, tmp, tmp_bytes, total;
+};
+
+size_t al(size_t x) { return (x + 255) / 256 * 256; }
+
+int nms_layout(int B, int A, int K, NmsLayout* L) {
+  const size_t n = (size_t)B * A;
+  size_t tmp_bytes = 0;
+  hipError_t e = rocprim::segmented_radix_sort_pairs_desc(
+      nullptr, tmp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, rocprim::counting_iterator<int>(0),
+      (int*)nullptr, (unsigned)n, (unsigned)B, (const int*)nullptr, (const int*)nullptr, 0, 32, (hipStream_t)0);
+  if (e != hipSuccess) {
+    set_error(std::string("fast_nms: sort workspace query: ") + hipGetErrorString(e));
+    return 3;
+  }
+  size_t o = 0;
+  L->keys = o;  o += al(n * 4);
+  L->skeys = o; o += al(n * 4);
+  L->sidx = o;  o += al(n * 4);
+  L->keep = o;  o += al((size_t)B * K);
+  L->offs = o;  o += al((size_t)(B + 1) * 4);
+  L->tmp = o;   o += al(tmp_bytes);
+  L->tmp_bytes = tmp_bytes;
+  L->total = o;
+  return 0;
+}
+
+}  // namespace
+
+size_t yolact_nms_workspace_bytes(int B, int A, int top_k) {
+  NmsLayout L{};
+  if (B < 1 || A < 1 || top_k < 1 || nms_layout(B, A, std::min(top_k, A), &L)) return 0;
+  return L.total;
+}
+
+int launch_yolact_fast_nms(const float* cls, long long cls_bstride, int A, int C1, const float* box,
+                           long long box_bstride, int B, int top_k, float iou_thr, float conf_thr, void* ws,
+                           size_t ws_bytes, long long* det, int det_stride, int* n_det, hipStream_t s) {
+  if (A < 1 || B < 1 || C1 < 2 || top_k < 1 || (long long)B * A >= (1LL << 31)) {
+    set_error("fast_nms: need anchors >= 1, >= 2 classes (incl. background), top_k >= 1");
+    return 2;  // TV_ESHAPE
+  }
+  const int K = std::min(top_k, A);
+  if (det_stride < K) { set_error("fast_nms: det row stride < min(top_k, anchors)"); return 1; }
+  NmsLayout L{};
+  int rc = nms_layout(B, A, K, &L);
+  if (rc) return rc;
+  if (!ws || ws_bytes < L.total) { set_error("fast_nms: workspace too small"); return 1; }
+  char* w = (char*)ws;
+  uint32_t* keys = (uint32_t*)(w + L.keys);
+  uint32_t* skeys = (uint32_t*)(w + L.skeys);
+  int* sidx = (int*)(w + L.sidx);
+  uint8_t* keep = (uint8_t*)(w + L.keep);
+  int* offs = (int*)(w + L.offs);
+  const unsigned n = (unsigned)B * A;
+  hipLaunchKernelGGL(yolact::nms_keys, dim3((n + 255) / 256), dim3(256), 0, s, cls, cls_bstride, A, C1, B, keys);
+  TV_HIP(hipGetLastError());
+  hipLaunchKernelGGL(yolact::segment_offsets, dim3((B + 256) / 256), dim3(256), 0, s, offs, B, A);
+  TV_HIP(hipGetLastError());
+  size_t tb = L.tmp_bytes;
+  TV_HIP(rocprim::segmented_radix_sort_pairs_desc(w + L.tmp, tb, keys, skeys, rocprim::counting_iterator<int>(0),
+                                                  sidx, n, (unsigned)B, offs, offs + 1, 0, 32, s));
+  hipLaunchKernelGGL(yolact::nms_iou, dim3((K + yolact::kIouThreads - 1) / yolact::kIouThreads, B),
+                     dim3(yolact::kIouThreads), 0, s, box, box_bstride, A, K, skeys, sidx, iou_thr, conf_thr, keep);
+  TV_HIP(hipGetLastError());
+  hipLaunchKernelGGL(yolact::nms_compact, dim3(B), dim3(yolact::kCompactThreads), 0, s, keep, A, K, sidx, det,
+                     det_stride, n_det);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch_yolact_assemble_mask(const float* proto, const long long pst[4], int B, int K, int H, int W,
+                                const float* coeff, const float* box, const int* counts, int n_max, float* out,
+                                hipStream_t s) {
+  if (B < 1 || K < 1 || H < 1 || W < 1 || n_max < 0 || (long)H * W >= (1L << 30) || B > 65535) {
     set_error("assemble_mask: bad shapes");
     return 2;  // TV_ESHAPE
   }
-  if (n == 0) return 0;
-  const unsigned t = (unsigned)n * H * W;
-  hipLaunchKernelGGL(yolact::assemble_mask, dim3((t + 255) / 256), dim3(256), 0, s, proto, K, H, W, coeff, box, n,
-                     out);
+  if (n_max == 0) return 0;
+  const size_t lds = (size_t)K * yolact::kMaskPix * sizeof(float);
+  if (lds > 160 * 1024) { set_error("assemble_mask: more than 40 prototypes"); return 2; }
+  static std::once_flag attr_once;
+  hipError_t attr_err = hipSuccess;
+  std::call_once(attr_once, [&] {
+    attr_err = hipFuncSetAttribute((const void*)yolact::assemble_mask, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   160 * 1024);
+  });
+  TV_HIP(attr_err);
+  yolact::MaskParams p{proto, pst[0], pst[1], pst[2], pst[3], K, H, W, coeff, box, counts, n_max, out};
+  const int hw = H * W;
+  hipLaunchKernelGGL(yolact::assemble_mask, dim3((hw + yolact::kMaskPix - 1) / yolact::kMaskPix, B),
+                     dim3(yolact::kMaskThreads), lds, s, p);
   TV_HIP(hipGetLastError());
   return 0;
 }

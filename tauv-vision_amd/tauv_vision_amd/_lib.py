@@ -54,8 +54,15 @@ EXPORTS = {
                    ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_f32, c_vp,
                    ctypes.POINTER(c_i64), c_vp, c_vp, c_vp, c_i64, c_vp], c_i32),
     "tv_yolact_box_decode": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp], c_i32),
+    "tv_yolact_box_encode": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_f32, c_f32, c_vp, c_vp], c_i32),
     "tv_yolact_fast_nms": ([c_vp, c_i32, c_i32, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp, c_vp], c_i32),
-    "tv_yolact_assemble_mask": ([c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
+    "tv_yolact_nms_workspace_size": ([c_i32, c_i32, c_i32, ctypes.POINTER(c_i64)], c_i32),
+    "tv_yolact_fast_nms_batched": ([c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_f32, c_f32, c_vp, c_vp, c_vp, c_i64,
+                                    c_vp], c_i32),
+    "tv_yolact_assemble_mask": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
+                                c_i32),
+    "tv_yolact_assemble_masks": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32,
+                                  c_vp, c_vp], c_i32),
     "tv_last_error": ([], ctypes.c_char_p),
     "tv_version": ([], ctypes.c_char_p),
 }

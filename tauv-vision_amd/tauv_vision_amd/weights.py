@@ -8,7 +8,7 @@ import torch
 from . import _lib
 
 
-ARCH_CENTERNET, ARCH_DLA34 = 0, 1
+ARCH_CENTERNET, ARCH_DLA34, ARCH_PROTONET = 0, 1, 2
 
 
 def model_desc(heights, channels, downsamples, head_channels, in_h=64, in_w=64, precision="fp32",
@@ -38,6 +38,11 @@ def model_desc(heights, channels, downsamples, head_channels, in_h=64, in_w=64, 
 def dla34_desc(head_channels, in_h=64, in_w=64, precision="fp32"):
     """CenterpointDLA34 (centerpoint_dla.py:544-578): the DLA-34 structure is fixed."""
     return model_desc([], [16], 2, head_channels, in_h, in_w, precision, arch=ARCH_DLA34)
+
+
+def protonet_desc(feature_depth, n_prototype_masks, fpn_h=8, fpn_w=8, precision="fp32"):
+    """YOLACT Masknet (masknet.py:8-55) over an fpn[0] map of fpn_h x fpn_w."""
+    return model_desc([], [feature_depth], 0, [n_prototype_masks], fpn_h, fpn_w, precision, arch=ARCH_PROTONET)
 
 
 def param_layout(desc):

@@ -55,6 +55,52 @@ DLA34_CASES = [
          objects={"n_labels": 4, "keypoints_per_label": 1}),
 ]
 
+# YOLACT Masknet protonet (masknet.py:8-55): feature_depth F, n_prototype_masks k, fpn[0] size.
+# Small cases store the full output; the production-size cases (train.py:28-33 config F=256, k=8
+# at the 640x360 fpn[0] of 45x80 and BASELINE's 550x550 -> 69x69) store a seeded sample of output
+# positions plus per-channel float64 sums, and the tests regenerate inputs / weights from the seeds.
+PROTONET_CASES = [
+    dict(name="protonet_f32_k8_b2_12x20", F=32, k=8, batch=2, H=12, W=20, seed=310, full=True),
+    dict(name="protonet_f64_k16_b1_9x17", F=64, k=16, batch=1, H=9, W=17, seed=311, full=True),
+    dict(name="protonet_f256_k8_b1_45x80", F=256, k=8, batch=1, H=45, W=80, seed=312, full=False),
+    dict(name="protonet_f256_k8_b1_69x69", F=256, k=8, batch=1, H=69, W=69, seed=313, full=False),
+]
+PROTONET_SAMPLES = 4096
+
+
+def protonet_case(name):
+    for c in PROTONET_CASES:
+        if c["name"] == name:
+            return c
+    raise KeyError(name)
+
+
+def protonet_layout(F, k):
+    """masknet.py:13-41 registration order (the reference Masknet.state_dict() keys)."""
+    out = []
+    for i, up in ((1, True), (2, True), (3, False)):
+        out += [(f"_layers_{i}.0.0.weight", (F, F, 3, 3)), (f"_layers_{i}.0.0.bias", (F,))]
+        if up:
+            out += [(f"_upsample_layer_{i}.weight", (F, F, 3, 3)), (f"_upsample_layer_{i}.bias", (F,))]
+    out += [("_output_layer.weight", (k, F, 1, 1)), ("_output_layer.bias", (k,))]
+    return out
+
+
+def protonet_inputs(case):
+    """(state_dict, fpn[0] input [B, F, H, W]) of a protonet case."""
+    sd = seeded_state_dict(protonet_layout(case["F"], case["k"]), conv_seed=case["seed"], aux_seed=case["seed"] + 1)
+    g = torch.Generator().manual_seed(case["seed"] + 2)
+    x = torch.randn((case["batch"], case["F"], case["H"], case["W"]), generator=g)
+    return sd, x
+
+
+def protonet_sample_index(case):
+    """Seeded flat output positions of the sampled (full=False) cases."""
+    B, k, Ho, Wo = case["batch"], case["k"], 4 * case["H"], 4 * case["W"]
+    g = torch.Generator().manual_seed(case["seed"] + 3)
+    return torch.randint(0, B * k * Ho * Wo, (PROTONET_SAMPLES,), generator=g)
+
+
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 

@@ -1,14 +1,18 @@
-"""YOLACT post-processing: the CPU oracle pinned to the reference's goldens
-(tests/golden/gen_golden_yolact.py), and the HIP kernels (csrc/yolact.hip) against the same.
+"""YOLACT protonet + post-processing: the CPU oracle pinned to the reference's
+goldens (tests/golden/gen_golden_yolact.py), and the HIP path (csrc/yolact.hip, the protonet
+engine) against the same.
 
-Bars: anchors, NMS indices and the box mask are exact; box_decode within 2 ulp-scale (device
-expf vs the host's vectorised exp); masks within 1e-6 (sigmoid of an 8-term fp32 sum)."""
+Bars: anchors, NMS indices and the box mask are exact; box_decode / box_encode within 2 ulp-scale
+(device expf / logf vs the host's vectorised exp / log); masks within 1e-6 (sigmoid of a k-term
+fp32 sum); the fp32 protonet within 1e-4 of the reference (the north star's fp32 bar), fp16 / bf16
+within ~3x the drift measured on MI355X (profiles/r2/parity_lowp.json)."""
 import numpy as np
 import pytest
 import torch
 
-from helpers import golden
+from helpers import golden, record_measurement
 from oracle import ref_yolact as ry
+from recipe import PROTONET_CASES, protonet_case, protonet_inputs, protonet_layout
 
 CASES = {
     "yolact_640x360": dict(in_w=640, in_h=360, fpn=[(45, 80), (23, 40), (12, 20), (6, 10), (3, 5)], ars=(1,)),
@@ -36,11 +40,63 @@ def test_oracle_matches_reference(name):
     for k, iou, conf in NMS_KEYS:
         np.testing.assert_array_equal(ry.nms(_t(g["cls"]), box, k, iou, conf).numpy(), g[f"nms_{k}_{iou}_{conf}"])
     det = _t(g["mask_det"])
-    coeff, proto = _t(g["coeff"]), _t(g["proto"])
-    np.testing.assert_allclose(ry.assemble_mask(proto, coeff[0, det[:24]], box[0, det[:24]]).numpy(), g["mask_box"],
+    cb, cn = _mask_coeffs(g)
+    proto = _t(g["proto"])
+    np.testing.assert_allclose(ry.assemble_mask(proto, cb, box[0, det[:24]]).numpy(), g["mask_box"],
                                rtol=0, atol=1e-6)
-    np.testing.assert_allclose(ry.assemble_mask(proto, coeff[0, det[:5]], None).numpy(), g["mask_nobox"], rtol=0,
-                               atol=1e-6)
+    np.testing.assert_allclose(ry.assemble_mask(proto, cn, None).numpy(), g["mask_nobox"], rtol=0, atol=1e-6)
+
+
+def _mask_coeffs(g):
+    """Coefficient rows of the stored masks (the first 24 / 5 kept detections)."""
+    if "coeff_box" in g:
+        return _t(g["coeff_box"]), _t(g["coeff_nobox"])
+    det = _t(g["mask_det"])
+    coeff = _t(g["coeff"])
+    return coeff[0, det[:24]], coeff[0, det[:5]]
+
+
+def _nms_keys(g):
+    return [tuple(float(v) if "." in v else int(v) for v in k.split("_")[1:]) for k in g if k.startswith("nms_")]
+
+
+def test_oracle_large_and_degenerate_nms_match_reference():
+    g = golden("yolact_640x360_ar3")
+    assert int(g["A"]) == 14505  # evaluate.py:17-34: 4835 cells x 3 aspect ratios
+    for k, iou, conf in _nms_keys(g):
+        np.testing.assert_array_equal(ry.nms(_t(g["cls"]), _t(g["box"]), k, iou, conf).numpy(),
+                                      g[f"nms_{k}_{iou}_{conf}"])
+    d = golden("yolact_degenerate")
+    for k, iou, conf in _nms_keys(d):
+        np.testing.assert_array_equal(ry.nms(_t(d["cls"]), _t(d["box"]), k, iou, conf).numpy(),
+                                      d[f"nms_{k}_{iou}_{conf}"])
+
+
+def test_oracle_box_encode_matches_reference():
+    g = golden("yolact_640x360_ar3")
+    enc = ry.box_encode(_t(g["gt_box"]), _t(g["anchor"]), VAR)
+    np.testing.assert_allclose(enc.numpy(), g["gt_enc"], rtol=4e-7, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in PROTONET_CASES])
+def test_oracle_protonet_matches_reference(name):
+    c, g = protonet_case(name), golden(name)
+    sd, x = protonet_inputs(c)
+    with torch.no_grad():
+        y = ry.masknet(sd, x)
+    assert tuple(y.shape) == tuple(g["out_shape"])
+    if c["full"]:
+        np.testing.assert_array_equal(y.numpy(), g["out"])
+    else:
+        np.testing.assert_array_equal(y.reshape(-1)[_t(g["sample_index"])].numpy(), g["sample"])
+    np.testing.assert_allclose(y.double().sum(dim=(0, 2, 3)).numpy(), g["chan_sum"], rtol=1e-9)
+
+
+def test_masknet_layout_matches_reference():
+    from tauv_vision_amd.yolact import Masknet, YolactConfig
+    for F, k in ((256, 8), (32, 32), (64, 16)):
+        m = Masknet(YolactConfig(640, 360, SCALES, (1,), VAR, feature_depth=F, n_prototype_masks=k))
+        assert [(n, tuple(v.shape)) for n, v in m.state_dict().items()] == protonet_layout(F, k)
 
 
 def test_drop_in_get_anchor_matches_reference():
@@ -68,13 +124,16 @@ def test_gpu_postprocess_matches_reference(name):
         np.testing.assert_array_equal(nms(cls, _t(ref_box).cuda(), k, iou, conf).cpu().numpy(), ref)
         np.testing.assert_array_equal(nms(cls, box, k, iou, conf).cpu().numpy(), ref)
     det = _t(g["mask_det"])
-    coeff, proto = _t(g["coeff"]).cuda(), _t(g["proto"]).cuda()
+    cb, cn = (c.cuda() for c in _mask_coeffs(g))
+    proto = _t(g["proto"]).cuda()
     rb = _t(ref_box).cuda()
-    m = assemble_mask(proto, coeff[0, det[:24]], rb[0, det[:24]]).cpu().numpy()
+    m = assemble_mask(proto, cb, rb[0, det[:24]]).cpu().numpy()
     np.testing.assert_allclose(m, g["mask_box"], rtol=0, atol=1e-6)
     assert ((m == 0) == (g["mask_box"] == 0)).all()  # the inclusive box mask is exact
-    np.testing.assert_allclose(assemble_mask(proto, coeff[0, det[:5]], None).cpu().numpy(), g["mask_nobox"], rtol=0,
-                               atol=1e-6)
+    np.testing.assert_allclose(assemble_mask(proto, cn, None).cpu().numpy(), g["mask_nobox"], rtol=0, atol=1e-6)
+    # the same prototypes read through an NHWC view (Masknet's output layout)
+    nhwc = proto.permute(1, 2, 0).contiguous().permute(2, 0, 1)
+    np.testing.assert_array_equal(assemble_mask(nhwc, cb, rb[0, det[:24]]).cpu().numpy(), m)
 
 
 @pytest.mark.gpu
@@ -88,5 +147,104 @@ def test_gpu_postprocess_edge_cases():
     assert nms(torch.randn(1, 1, 3).cuda(), box[:, :1], 100, 0.5, 0.0).tolist() == [0]
     # zero detections -> [0, H, W]
     assert assemble_mask(torch.rand(4, 8, 8).cuda(), torch.zeros(0, 4).cuda(), None).shape == (0, 8, 8)
-    with pytest.raises(RuntimeError):  # the one-workgroup kernel's documented limit (8192 anchors)
-        nms(torch.randn(1, 9000, 3).cuda(), torch.rand(1, 9000, 4).cuda(), 10, 0.5, 0.1)
+    # more anchors than one workgroup's LDS holds (the reference has no limit)
+    g = torch.Generator().manual_seed(5)
+    cls9, box9 = torch.randn(1, 30000, 3, generator=g), torch.rand(1, 30000, 4, generator=g) * 0.3
+    np.testing.assert_array_equal(nms(cls9.cuda(), box9.cuda(), 300, 0.5, 0.1).cpu().numpy(),
+                                  ry.nms(cls9, box9, 300, 0.5, 0.1).numpy())
+
+
+@pytest.mark.gpu
+def test_gpu_large_and_degenerate_nms():
+    from tauv_vision_amd.yolact import nms, BatchedNMS
+    for name in ("yolact_640x360_ar3", "yolact_degenerate"):
+        g = golden(name)
+        cls, box = _t(g["cls"]).cuda(), _t(g["box"]).cuda()
+        for k, iou, conf in _nms_keys(g):
+            np.testing.assert_array_equal(nms(cls, box, k, iou, conf).cpu().numpy(), g[f"nms_{k}_{iou}_{conf}"])
+    # batched: every image of a batch == the reference nms of that image alone
+    g = golden("yolact_550x550")
+    cls, box = _t(g["cls"]), _t(g["box"])
+    bn = BatchedNMS(cls.shape[0], cls.shape[1], 100, "cuda")
+    det, cnt = bn(cls.cuda(), box.cuda(), 0.5, 0.05)
+    det, cnt = det.cpu().numpy(), cnt.cpu().numpy()
+    for b in range(cls.shape[0]):
+        ref = ry.nms(cls[b:b + 1], box[b:b + 1], 100, 0.5, 0.05).numpy()
+        assert cnt[b] == len(ref)
+        np.testing.assert_array_equal(det[b, :cnt[b]], ref)
+
+
+@pytest.mark.gpu
+def test_gpu_box_encode_matches_reference():
+    from tauv_vision_amd.yolact import YolactConfig, box_encode, box_decode
+    g = golden("yolact_640x360_ar3")
+    cfg = YolactConfig(640, 360, SCALES, (0.5, 1, 2), VAR)
+    anchor = _t(g["anchor"]).cuda()
+    enc = box_encode(_t(g["gt_box"]).cuda(), anchor, cfg)
+    np.testing.assert_allclose(enc.cpu().numpy(), g["gt_enc"], rtol=4e-7, atol=2e-7)
+    # decode(encode(box)) == box (the round trip of boxes.py:106-117)
+    np.testing.assert_allclose(box_decode(enc, anchor, cfg).cpu().numpy(), g["gt_box"], rtol=2e-6, atol=2e-7)
+
+
+@pytest.mark.gpu
+def test_gpu_assemble_masks_batched():
+    from tauv_vision_amd.yolact import assemble_mask, assemble_masks
+    g = torch.Generator().manual_seed(9)
+    B, K, H, W, n = 3, 8, 37, 53, 11
+    proto = torch.randn(B, H, W, K, generator=g).cuda().permute(0, 3, 1, 2)  # NHWC storage
+    coeff = torch.randn(B, n, K, generator=g).cuda()
+    box = torch.cat([torch.rand(B, n, 2, generator=g), torch.rand(B, n, 2, generator=g) * 0.6], -1).cuda()
+    counts = torch.tensor([11, 0, 5], dtype=torch.int32).cuda()
+    out = assemble_masks(proto, coeff, box, counts, out=torch.full((B, n, H, W), -1.0).cuda()).cpu()
+    for b in range(B):
+        c = int(counts[b])
+        if c:
+            np.testing.assert_array_equal(out[b, :c].numpy(), assemble_mask(proto[b], coeff[b, :c], box[b, :c]).cpu().numpy())
+            ref = ry.assemble_mask(proto[b].cpu(), coeff[b, :c].cpu(), box[b, :c].cpu()).numpy()
+            np.testing.assert_allclose(out[b, :c].numpy(), ref, rtol=0, atol=1e-6)
+        assert (out[b, c:] == -1.0).all()  # rows past the count untouched
+
+
+PROTO_TOL = {"fp32": 1e-4, "fp16": 8e-4, "bf16": 6e-3}  # ~3x the MI355X drift (profiles/r2/parity_yolact.json)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp32", "fp16", "bf16"])
+@pytest.mark.parametrize("name", [c["name"] for c in PROTONET_CASES])
+def test_gpu_protonet_matches_reference(name, precision):
+    from tauv_vision_amd.yolact import Masknet, YolactConfig
+    c, g = protonet_case(name), golden(name)
+    sd, x = protonet_inputs(c)
+    m = Masknet(YolactConfig(640, 360, SCALES, (1,), VAR, feature_depth=c["F"], n_prototype_masks=c["k"]),
+                precision=precision)
+    m.load_state_dict(sd)
+    y = m(x.cuda())
+    assert tuple(y.shape) == tuple(g["out_shape"])
+    y = y.cpu()
+    if c["full"]:
+        err = float(np.abs(y.numpy() - g["out"]).max())
+        scale = float(np.abs(g["out"]).max())
+    else:
+        got = y.reshape(-1)[_t(g["sample_index"])].numpy() if y.is_contiguous() else \
+            y.contiguous().reshape(-1)[_t(g["sample_index"])].numpy()
+        err = float(np.abs(got - g["sample"]).max())
+        scale = float(np.abs(g["sample"]).max())
+    record_measurement(f"protonet/{name}/{precision}", {"max_abs_err": err, "ref_absmax": scale})
+    assert err <= PROTO_TOL[precision] * max(1.0, scale), f"{name} {precision}: {err}"
+    np.testing.assert_allclose(y.double().sum(dim=(0, 2, 3)).numpy(), g["chan_sum"],
+                               rtol=PROTO_TOL[precision] * 10)
+
+
+@pytest.mark.gpu
+def test_gpu_protonet_batch_consistency():
+    """Frames are independent: a batch (incl. the two concurrent slices of B >= 16) gives every
+    frame exactly its single-frame result."""
+    from tauv_vision_amd.yolact import Masknet, YolactConfig
+    c = protonet_case("protonet_f64_k16_b1_9x17")
+    sd, _ = protonet_inputs(c)
+    m = Masknet(YolactConfig(640, 360, SCALES, (1,), VAR, feature_depth=64, n_prototype_masks=16), precision="fp16")
+    m.load_state_dict(sd)
+    x = torch.randn(17, 64, 9, 17, generator=torch.Generator().manual_seed(4)).cuda()
+    yb = m(x).cpu()
+    for i in (0, 8, 16):
+        np.testing.assert_array_equal(m(x[i:i + 1]).cpu().numpy(), yb[i:i + 1].numpy())

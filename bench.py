@@ -363,6 +363,137 @@ def cpu_baseline(sd, seconds, K, thr, arch="r18"):
                       f"oracle/ PyTorch-CPU restatement, bit-identical to the reference on CPU"}
 
 
+YOLACT_METRIC = "frames/sec YOLACT protonet + box decode + fast NMS + mask assembly 550x550 batch=32 + %roofline"
+
+
+def run_yolact(args, world, rank, device):
+    """BASELINE config 5 (YOLACT 550x550, batch 32): one step = fpn[0] [B, 256, 69, 69] resident
+    in HBM -> Masknet protonet (masknet.py:8-55; F = 256, k = 8 prototypes, train.py:28-33) ->
+    box_decode of every anchor (boxes.py:55-61; 6416 anchors at 550x550) -> fast NMS per image
+    (nms.py:7-29; top_k 100 as evaluate_batch.py:51, IoU 0.5, confidence 0.05) -> assemble_mask
+    of the kept detections (masks.py:8-21, at prototype resolution 276x276) -> counts to host.
+    The ResNet backbone / FPN / prediction head are not on the north-star path (they need
+    torchvision, absent here): their outputs are synthetic tensors of the reference's shapes."""
+    from tauv_vision_amd.yolact import (Masknet, YolactConfig, BatchedNMS, box_decode, get_anchor,
+                                        assemble_masks_indexed)
+    B, F, k, C1 = args.batch if args.batch != 64 else 32, 256, 8, 8
+    cfg = YolactConfig(550, 550, (24, 48, 96, 192, 384), (1,), (0.1, 0.2), feature_depth=F, n_prototype_masks=k)
+    fpn = [(69, 69), (35, 35), (18, 18), (9, 9), (5, 5)]
+    anchor = torch.cat([get_anchor(i, s, cfg) for i, s in enumerate(fpn)], 1).to(device)
+    A = anchor.shape[1]
+    top_k = 100
+    net = Masknet(cfg, precision=args.precision)
+    g = torch.Generator(device=device).manual_seed(2000 + rank)
+    x = torch.randn((B, F, 69, 69), generator=g, device=device)
+    cls = torch.randn((B, A, C1), generator=g, device=device) * 2.0
+    enc = torch.randn((B, A, 4), generator=g, device=device) * 0.5
+    coeff = torch.randn((B, A, k), generator=g, device=device)
+    eng = net.engine(device, 69, 69)
+    eng.prepare(B)
+    proto = eng.alloc_out(B)                       # [B, 276, 276, 8] fp32 NHWC
+    pview = proto[..., :k].permute(0, 3, 1, 2)     # the reference's [B, k, 276, 276]
+    bnms = BatchedNMS(B, A, top_k, device)
+    masks = torch.empty((B, bnms.K, 276, 276), dtype=torch.float32, device=device)
+    host_counts = torch.empty((B,), dtype=torch.int32, pin_memory=True)
+    box_out = {}
+
+    def step():
+        eng.forward(x, proto)
+        box_out["box"] = box = box_decode(enc, anchor, cfg)
+        det, cnt = bnms(cls, box, 0.5, 0.05)
+        assemble_masks_indexed(pview, coeff, box, det, cnt, out=masks)
+        host_counts.copy_(cnt, non_blocking=True)
+
+    elapsed = timed(step, args.steps, args.warmup, world, device)
+    value = world * B * args.steps / elapsed
+    flops_frame = eng.geom["flops_per_frame"]
+
+    # dominant protonet kernel (per-launch HIP events) and the mask kernel's HBM rate
+    prof = eng.profile(x, proto)
+    kern = {}
+    for lab, ms, fl, kname in prof:
+        if fl > 0:
+            kk = kern.setdefault(kname, [0, 0.0, 0.0])
+            kk[0] += 1
+            kk[1] += ms
+            kk[2] += fl
+    name, (n, ms, fl) = max(kern.items(), key=lambda kv: kv[1][1])
+    peak = PEAK_TFLOPS[args.precision]
+    roof = {"bound": "mfma", "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4), "traffic": None, "launch_batch": B,
+            "kernel": f"{name}: {n} launches/forward, avg {ms / n:.4f} ms, avg {fl / n / 1e9:.2f} GFLOP/launch",
+            "per_kernel": {kn: {"launches": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / v[1] / 1e9, 1)}
+                           for kn, v in kern.items()},
+            "protonet_ms": round(sum(o[1] for o in prof), 4)}
+    s = torch.cuda.current_stream(device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    box = box_out["box"]
+    det, cnt = bnms(cls, box, 0.5, 0.05)
+    best = None
+    for _ in range(10):
+        ev[0].record(s)
+        assemble_masks_indexed(pview, coeff, box, det, cnt, out=masks)
+        ev[1].record(s)
+        ev[1].synchronize()
+        t = ev[0].elapsed_time(ev[1])
+        best = t if best is None else min(best, t)
+    kept = int(cnt.sum())
+    nbytes = kept * 276 * 276 * 4 + B * 276 * 276 * k * 4 + kept * (k + 4) * 4
+    mask_roof = {"bound": "hbm", "achieved": round(nbytes / (best * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                 "unit": "GB/s", "frac": round(nbytes / (best * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                 "ms": round(best, 4), "bytes": nbytes, "masks": kept}
+    ev0 = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    best_nms = None
+    for _ in range(10):
+        ev0[0].record(s)
+        bx = box_decode(enc, anchor, cfg)
+        bnms(cls, bx, 0.5, 0.05)
+        ev0[1].record(s)
+        ev0[1].synchronize()
+        t = ev0[0].elapsed_time(ev0[1])
+        best_nms = t if best_nms is None else min(best_nms, t)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        from oracle import ref_yolact as ry
+        sd = {kk: v.detach().cpu() for kk, v in net.state_dict().items()}
+        xc, clc, bxc, cfc = x[:1].cpu(), cls[:1].cpu(), box[:1].cpu(), coeff[:1].cpu()
+        nfr, t0 = 0, time.perf_counter()
+        with torch.no_grad():
+            while True:
+                pr = ry.masknet(sd, xc)
+                bb = ry.box_decode(enc[:1].cpu(), anchor.cpu(), cfg.box_variances)
+                d = ry.nms(clc, bb, top_k, 0.5, 0.05)
+                ry.assemble_mask(pr[0], cfc[0, d], bb[0, d])
+                nfr += 1
+                el = time.perf_counter() - t0
+                if el >= args.cpu_seconds:
+                    break
+        cpu = {"value": round(nfr / el, 4), "unit": "frames/sec", "cores": torch.get_num_threads(), "kind": "port",
+               "cpu_model": cpu_model(),
+               "sample": f"{nfr} single frames (B=1): fp32 protonet + box_decode + nms + assemble_mask in {el:.1f}s; "
+                         f"oracle/ PyTorch-CPU restatement, bit-identical to the reference on CPU"}
+    if rank == 0:
+        line = {
+            "metric": YOLACT_METRIC, "value": round(value, 2), "unit": "frames/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic",
+            "config": {"workload": f"YOLACT 550x550: Masknet protonet (F={F}, k={k}) on fpn[0] 69x69 -> protos "
+                                   f"276x276, box_decode of {A} anchors, fast NMS (top_k {top_k}, IoU 0.5, conf 0.05) "
+                                   f"per frame, assemble_mask of the kept detections; batch={B}/GPU",
+                       "global_batch": B * world, "parallelism": f"dp{world}"},
+            "e2e_tflops": round(value * flops_frame / 1e12, 2),
+            "e2e_frac_of_peak": round(value * flops_frame / 1e12 / peak, 4),
+            "roofline": roof, "mask_roofline": mask_roof, "nms_ms": round(best_nms, 4),
+            "detections_per_frame": round(kept / B, 2), "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def env_knobs():
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("TV_")}
 
@@ -383,8 +514,9 @@ def main():
     ap.add_argument("--b1-steps", type=int, default=200)
     ap.add_argument("--fp32-steps", type=int, default=3)
     ap.add_argument("--allow-env-knobs", action="store_true")
-    ap.add_argument("--model", default="r18", choices=["r18", "dla34"],
-                    help="r18: the BASELINE CenterNet-R18 (headline); dla34: CenterpointDLA34, heads [4,4,8,2,2]")
+    ap.add_argument("--model", default="r18", choices=["r18", "dla34", "yolact"],
+                    help="r18: the BASELINE CenterNet-R18 (headline); dla34: CenterpointDLA34, heads [4,4,8,2,2]; "
+                         "yolact: protonet + post-processing at 550x550, batch 32 (BASELINE config 5)")
     args = ap.parse_args()
     knobs = env_knobs()
     if knobs and not args.allow_env_knobs:
@@ -397,6 +529,9 @@ def main():
     device = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
+
+    if args.model == "yolact":
+        return run_yolact(args, world, rank, device)
 
     H, W, B, K = 480, 640, args.batch, args.k
     model, oc, sd = build_model(args.precision, device, args.model)

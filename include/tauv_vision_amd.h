@@ -168,7 +168,7 @@ int tv_yolact_fast_nms_batched(const float* classification, int32_t B, int32_t A
                                int64_t* det, int32_t* n_det, void* workspace, int64_t workspace_bytes, void* stream);
 /* assemble_mask (masks.py:8-21): prototypes [K,H,W] at element strides proto_strides (k, y, x) —
  * contiguous NCHW or the protonet's NHWC output view —, coefficients [n,K], box [n,4] (y, x, h, w
- * normalised) or NULL -> mask [n,H,W] = sigmoid(coeff . proto) x inclusive box mask. K <= 40. */
+ * normalised) or NULL -> mask [n,H,W] = sigmoid(coeff . proto) x inclusive box mask. K <= 37. */
 int tv_yolact_assemble_mask(const float* mask_prototype, const int64_t proto_strides[3], int32_t K, int32_t H,
                             int32_t W, const float* mask_coeff, const float* box, int32_t n, float* mask,
                             void* stream);
@@ -178,6 +178,14 @@ int tv_yolact_assemble_mask(const float* mask_prototype, const int64_t proto_str
 int tv_yolact_assemble_masks(const float* mask_prototype, const int64_t proto_strides[4], int32_t B, int32_t K,
                              int32_t H, int32_t W, const float* mask_coeff, const float* box, const int32_t* counts,
                              int32_t n_max, float* mask, void* stream);
+/* The node's mask step straight from the batched NMS output (yolact_node.py:134:
+ * assemble_mask(proto[b], mask_coeff[b, det], box[b, det])): coefficients [B][A][K] and boxes
+ * [B][A][4] (or NULL) of every anchor, det [B][n_max] int64 kept anchors and counts [B] as written
+ * by tv_yolact_fast_nms_batched (n_max = its min(top_k, A)) -> masks [B][n_max][H][W]. */
+int tv_yolact_assemble_masks_indexed(const float* mask_prototype, const int64_t proto_strides[4], int32_t B,
+                                     int32_t K, int32_t H, int32_t W, const float* mask_coeff, const float* box,
+                                     int32_t A, const int64_t* det, const int32_t* counts, int32_t n_max, float* mask,
+                                     void* stream);
 
 const char* tv_last_error(void);
 const char* tv_version(void);

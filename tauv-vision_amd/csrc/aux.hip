@@ -132,6 +132,28 @@ int launch_nchw_to_nhwc(const float* img, int B, int C, int H, int W, void* out,
   });
 }
 
+// x = leaky_relu(x) in place over n fp32 values (the activation after a fused 1x1 whose channel
+// tiles were summed with atomics)
+__global__ void leaky_inplace(float4* __restrict__ x, size_t n4) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  float4 v = x[i];
+  v.x = fmaxf(v.x, 0.01f * v.x);
+  v.y = fmaxf(v.y, 0.01f * v.y);
+  v.z = fmaxf(v.z, 0.01f * v.z);
+  v.w = fmaxf(v.w, 0.01f * v.w);
+  x[i] = v;
+}
+
+int launch_leaky_inplace(float* x, size_t n, hipStream_t s) {
+  if (n % 4) { set_error("leaky_inplace: n must be a multiple of 4"); return 1; }
+  const size_t n4 = n / 4;
+  if (!n4) return 0;
+  hipLaunchKernelGGL(leaky_inplace, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, (float4*)x, n4);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
 // one thread per (target pixel, 16-byte chunk); covered rectangle [y0,y1) x [x0,x1) skipped
 __global__ void uncovered_copy(const uint4* __restrict__ add, int add_ldc16, uint4* __restrict__ out,
                                int out_ldc16, int chunks, int B, int tH, int tW, int y0, int y1, int x0, int x1) {

@@ -245,7 +245,8 @@ int tv_yolact_assemble_mask(const float* proto, const int64_t pst[3], int32_t K,
     if (n == 0) return TV_OK;
     if (!proto || !pst || !coeff || !mask || n < 0) { set_error("bad argument"); return TV_EINVAL; }
     const long long st[4] = {0, pst[0], pst[1], pst[2]};
-    return launch_yolact_assemble_mask(proto, st, 1, K, H, W, coeff, box, nullptr, n, mask, (hipStream_t)stream);
+    return launch_yolact_assemble_mask(proto, st, 1, K, H, W, coeff, box, nullptr, nullptr, 0, n, mask,
+                                       (hipStream_t)stream);
   })
 }
 
@@ -256,7 +257,23 @@ int tv_yolact_assemble_masks(const float* proto, const int64_t pst[4], int32_t B
     if (n_max == 0) return TV_OK;
     if (!proto || !pst || !coeff || !mask || n_max < 0) { set_error("bad argument"); return TV_EINVAL; }
     const long long st[4] = {pst[0], pst[1], pst[2], pst[3]};
-    return launch_yolact_assemble_mask(proto, st, B, K, H, W, coeff, box, counts, n_max, mask, (hipStream_t)stream);
+    return launch_yolact_assemble_mask(proto, st, B, K, H, W, coeff, box, counts, nullptr, 0, n_max, mask,
+                                       (hipStream_t)stream);
+  })
+}
+
+int tv_yolact_assemble_masks_indexed(const float* proto, const int64_t pst[4], int32_t B, int32_t K, int32_t H,
+                                     int32_t W, const float* coeff, const float* box, int32_t A, const int64_t* det,
+                                     const int32_t* counts, int32_t n_max, float* mask, void* stream) {
+  TV_GUARD({
+    if (n_max == 0) return TV_OK;
+    if (!proto || !pst || !coeff || !det || !counts || !mask || n_max < 0 || A < 1) {
+      set_error("bad argument");
+      return TV_EINVAL;
+    }
+    const long long st[4] = {pst[0], pst[1], pst[2], pst[3]};
+    return launch_yolact_assemble_mask(proto, st, B, K, H, W, coeff, box, counts, (const long long*)det, A, n_max,
+                                       mask, (hipStream_t)stream);
   })
 }
 

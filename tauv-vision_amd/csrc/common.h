@@ -83,7 +83,8 @@ int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int d
                      hipStream_t s);
 constexpr int kPipeTileM = 256;
 
-// Persistent halo-tile 3x3 / stride 1 / pad 1 kernel (conv3x3.hip), fp16/bf16: 512-pixel
+// Persistent halo-tile 3x3 / stride 1 / pad 1 kernel (conv3x3.hip), fp16/bf16, 128- or 256-channel
+// input (seg[0].C): 512-pixel
 // tiles of tw (16 or 32) columns; ConvParams.mtiles = conv3x3_tiles(B, H, W, tw); `grid`
 // persistent workgroups (one per CU, a multiple of 8 when >= 8).
 constexpr int kConv3MaxN = 1024;
@@ -102,8 +103,9 @@ size_t conv3x3s2_weight_bytes();
 int conv3x3s2_repack(const void* w, int Kpad, int esz, void* out, hipStream_t s);
 int launch_conv3x3s2(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int grid, hipStream_t s);
 // k-step-major, pre-swizzled weight copy the kernel streams (from the [Npad][Kpad] packing)
-size_t conv3x3_weight_bytes(int ntiles, int res);
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, void* out, hipStream_t s);
+// (ncb = input channel blocks of 32: 4 for 128-channel inputs, 8 for 256)
+size_t conv3x3_weight_bytes(int ntiles, int res, int ncb);
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, void* out, hipStream_t s);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
@@ -146,6 +148,8 @@ int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad,
                      hipStream_t s);
 int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cpad, int dtype,
                    hipStream_t s);
+// leaky_relu(0.01) in place over n fp32 values (n % 4 == 0)
+int launch_leaky_inplace(float* x, size_t n, hipStream_t s);
 // fp32 NCHW [B, C, H, W] -> NHWC compute dtype with pixel stride ldc (protonet input)
 int launch_nchw_to_nhwc(const float* img, int B, int C, int H, int W, void* out, int ldc, int dtype, hipStream_t s);
 // out[target] = add[target] for target pixels not covered by the shifted upsample.
@@ -171,9 +175,10 @@ size_t yolact_nms_workspace_bytes(int B, int A, int top_k);
 int launch_yolact_fast_nms(const float* cls, long long cls_bstride, int A, int C1, const float* box,
                            long long box_bstride, int B, int top_k, float iou_thr, float conf_thr, void* ws,
                            size_t ws_bytes, long long* det, int det_stride, int* n_det, hipStream_t s);
+// (det: [B][n_max] row of coefficients / boxes per detection among `rows` per image, or null)
 int launch_yolact_assemble_mask(const float* proto, const long long pst[4], int B, int K, int H, int W,
-                                const float* coeff, const float* box, const int* counts, int n_max, float* out,
-                                hipStream_t s);
+                                const float* coeff, const float* box, const int* counts, const long long* det,
+                                int rows, int n_max, float* out, hipStream_t s);
 int launch_uncovered_copy(const void* add, int add_ldc, void* out, int out_ldc, int C, int B,
                           int tH, int tW, int y0, int y1, int x0, int x1, int dtype,
                           hipStream_t s);

@@ -43,8 +43,9 @@ namespace c3 {
 constexpr int NT = 512, NW = 8, BN = 128, P = 512;
 constexpr int WP = P / NW;                    // pixels per wave = 64 (two 32-pixel fragments)
 constexpr int CBK = 32;                       // channels per k-step
-constexpr int NCB = 128 / CBK;                // channel blocks per tile (C == 128)
-template <int RES>
+// NCB: channel blocks per tile = C / 32 (4 for the 128-channel DLA levels, 8 for 256-channel inputs:
+// the YOLACT protonet's 3x3 convs, DLA-34's 256-channel level)
+template <int RES, int NCB = 4>
 constexpr int spt() { return (9 + RES) * NCB; }
 constexpr int PITCH = 80;                     // halo pixel pitch (bytes)
 constexpr int HPIX = 612;                     // (16+2)x(32+2) = (32+2)x(16+2) halo pixels
@@ -133,11 +134,12 @@ __device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh
 
 // NI: 32-channel fragments per wave — 4 (a 128-channel tile) or 2 (a 64-channel half tile, twice
 // the work units for layers whose 128-channel tiles leave the last round of CUs mostly idle)
-template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI>
+template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI, int NCB>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
   static_assert(NI == 4 || (NI == 2 && EPI == 0), "half tiles: plain epilogue only");
-  constexpr int SPTK = spt<RES>();  // k-steps per tile
+  static_assert(!RES || NCB == 4, "residual k-steps: 128-channel inputs only");
+  constexpr int SPTK = spt<RES, NCB>();  // k-steps per tile
   constexpr int BNK = 32 * NI;      // output channels per tile
   constexpr int WSL = BNK * 64;     // weight bytes per k-step (an LDS ring slot holds up to WSLOT)
   constexpr int WPL = WSL / 512;    // weight bytes per lane per k-step (16 or 8)
@@ -607,14 +609,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     if constexpr (RES) step(IC<9>{}, IC<false>{}, IC<(P0 + 9) & 3>{});
   };
 
-  // 4 channel blocks per tile, fully unrolled (36 k-steps of straight-line code): the
+  // NCB channel blocks per tile, fully unrolled (36 / 72 k-steps of straight-line code): the
   // accumulators keep one register assignment through the whole tile
-  static_assert(NCB == 4 && spt<0>() % 4 == 0 && spt<1>() % 4 == 0, "tile body: 4 channel blocks, k-steps per tile a multiple of the 4 weight register sets");
+  static_assert(NCB % 2 == 0 && SPTK % 4 == 0, "tile body: an even number of channel blocks (halo buffer parity), k-steps per tile a multiple of the 4 weight register sets");
+  auto blocks = [&](auto self, auto i) __attribute__((always_inline)) {
+    constexpr int I = decltype(i)::value;
+    if constexpr (I < NCB) {
+      cblock(IC<I>{});
+      self(self, IC<I + 1>{});
+    }
+  };
   for (; tl < ntl;) {
-    cblock(IC<0>{});
-    cblock(IC<1>{});
-    cblock(IC<2>{});
-    cblock(IC<3>{});
+    blocks(blocks, IC<0>{});
     epilogue(cur_fr, cur_y0, cur_x0, cur_nt);
     ++tl;
     if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
@@ -624,22 +630,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 // [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q][bnk rows][4 x 16 B] (channel tiles
 // of bnk = 128 or 64 rows), q = cb*9 + tap (res: q = cb*10 + j, j = 9 the residual segment's
 // channel block cb at K offset 9*128), slot s of row r holding chunk s ^ ((r >> 2) & 3) of the k-step
-__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, int res, int bnk,
+__global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntiles, int res, int bnk, int ncb,
                                uint4* __restrict__ out) {
-  const int sp = res ? spt<1>() : spt<0>();
+  const int sp = (9 + res) * ncb;
   const int n = ntiles * sp * BN * 4;  // ntiles of 128 rows
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
     const int slot = o & 3, row = (o >> 2) % bnk, q = (o / (4 * bnk)) % sp, nt = (o / (4 * bnk)) / sp;
     const int chunk = slot ^ ((row >> 2) & 3);
     const int cb = q / (9 + res), tap = q - cb * (9 + res);
-    const int k16 = (tap * 128 + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements); tap 9 = residual
+    const int k16 = (tap * CBK * ncb + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements); tap 9 = residual
     out[o] = w[(size_t)(nt * bnk + row) * kpad16 + k16];
   }
 }
 
-template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4>
+template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4, int NCB = 4>
 static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
-  auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI>;
+  auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>;
   constexpr int lds = lds_bytes<RES>();
   static bool attr = false;
   if (!attr) {
@@ -662,17 +668,18 @@ int conv3x3_tiles(int B, int H, int W, int tw) {
   return B * ((H + th - 1) / th) * ((W + tw - 1) / tw);
 }
 
-size_t conv3x3_weight_bytes(int ntiles, int res) {
-  return (size_t)ntiles * (res ? c3::spt<1>() : c3::spt<0>()) * c3::WSLOT;
+size_t conv3x3_weight_bytes(int ntiles, int res, int ncb) {
+  return (size_t)ntiles * (9 + res) * ncb * c3::WSLOT;
 }
 
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, void* out, hipStream_t s) {
-  if ((Kpad * esz) % 16 || Kpad < (res ? 10 : 9) * 128 || (ni != 4 && ni != 2)) {
-    set_error("conv3x3_repack: bad Kpad / ni");
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, void* out, hipStream_t s) {
+  if ((Kpad * esz) % 16 || Kpad < (9 + res) * 32 * ncb || (ni != 4 && ni != 2) || (ncb != 4 && ncb != 8) ||
+      (res && ncb != 4)) {
+    set_error("conv3x3_repack: bad Kpad / ni / channel blocks");
     return 1;
   }
   hipLaunchKernelGGL(c3::repack_weights, dim3(256), dim3(256), 0, s, (const uint4*)w, Kpad * esz / 16, ntiles, res,
-                     32 * ni, (uint4*)out);
+                     32 * ni, ncb, (uint4*)out);
   TV_HIP(hipGetLastError());
   return 0;
 }
@@ -684,12 +691,43 @@ int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dty
     set_error("conv3x3: bad activation / channel tile");
     return 1;
   }
+  const int ncb = p.seg[0].C / CBK;
+  if ((ncb != 4 && ncb != 8) || (ncb == 8 && res)) {
+    set_error("conv3x3: inputs of 128 or 256 channels (residual k-steps: 128)");
+    return 1;
+  }
+  using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
+  if (ncb == 8) {  // 256-channel inputs (protonet, DLA-34 level 4)
+    if (epi == 1) {
+      if (p.act != 2 || p.ntiles > 8) {
+        set_error("conv3x3: fused 1x1 needs LeakyReLU and <= 8 channel tiles");
+        return 1;
+      }
+      if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 2, 1, 0, 4, 8>(p, dp, out, grid, s) : launch_t<_Float16, 16, 2, 1, 0, 4, 8>(p, dp, out, grid, s);
+      if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 2, 1, 0, 4, 8>(p, dp, out, grid, s) : launch_t<__bf16, 16, 2, 1, 0, 4, 8>(p, dp, out, grid, s);
+      set_error("conv3x3: fp16/bf16 only");
+      return 1;
+    }
+    static const L f8[2][2][3] = {
+        {{launch_t<_Float16, 16, 0, 0, 0, 2, 8>, launch_t<_Float16, 16, 1, 0, 0, 2, 8>, launch_t<_Float16, 16, 2, 0, 0, 2, 8>},
+         {launch_t<_Float16, 32, 0, 0, 0, 2, 8>, launch_t<_Float16, 32, 1, 0, 0, 2, 8>, launch_t<_Float16, 32, 2, 0, 0, 2, 8>}},
+        {{launch_t<_Float16, 16, 0, 0, 0, 4, 8>, launch_t<_Float16, 16, 1, 0, 0, 4, 8>, launch_t<_Float16, 16, 2, 0, 0, 4, 8>},
+         {launch_t<_Float16, 32, 0, 0, 0, 4, 8>, launch_t<_Float16, 32, 1, 0, 0, 4, 8>, launch_t<_Float16, 32, 2, 0, 0, 4, 8>}}};
+    static const L b8[2][2][3] = {
+        {{launch_t<__bf16, 16, 0, 0, 0, 2, 8>, launch_t<__bf16, 16, 1, 0, 0, 2, 8>, launch_t<__bf16, 16, 2, 0, 0, 2, 8>},
+         {launch_t<__bf16, 32, 0, 0, 0, 2, 8>, launch_t<__bf16, 32, 1, 0, 0, 2, 8>, launch_t<__bf16, 32, 2, 0, 0, 2, 8>}},
+        {{launch_t<__bf16, 16, 0, 0, 0, 4, 8>, launch_t<__bf16, 16, 1, 0, 0, 4, 8>, launch_t<__bf16, 16, 2, 0, 0, 4, 8>},
+         {launch_t<__bf16, 32, 0, 0, 0, 4, 8>, launch_t<__bf16, 32, 1, 0, 0, 4, 8>, launch_t<__bf16, 32, 2, 0, 0, 4, 8>}}};
+    if (dtype == F16) return f8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
+    if (dtype == BF16) return b8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
+    set_error("conv3x3: fp16/bf16 only");
+    return 1;
+  }
   if (res) {  // ResidualBlock conv2 + conv_residual: ReLU, plain stores
     if (p.act != 1 || epi != 0 || p.nseg != 2 || p.ntiles != 1) {
       set_error("conv3x3: residual k-steps need ReLU, one channel tile and two segments");
       return 1;
     }
-    using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
     static const L r16[2][2] = {{launch_t<_Float16, 16, 1, 0, 1, 2>, launch_t<_Float16, 16, 1, 0, 1, 4>},
                                 {launch_t<_Float16, 32, 1, 0, 1, 2>, launch_t<_Float16, 32, 1, 0, 1, 4>}};
     static const L rb16[2][2] = {{launch_t<__bf16, 16, 1, 0, 1, 2>, launch_t<__bf16, 16, 1, 0, 1, 4>},
@@ -709,7 +747,6 @@ int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dty
     set_error("conv3x3: fp16/bf16 only");
     return 1;
   }
-  using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
   static const L f16[2][2][3] = {
       {{launch_t<_Float16, 16, 0, 0, 0, 2>, launch_t<_Float16, 16, 1, 0, 0, 2>, launch_t<_Float16, 16, 2, 0, 0, 2>},
        {launch_t<_Float16, 32, 0, 0, 0, 2>, launch_t<_Float16, 32, 1, 0, 0, 2>, launch_t<_Float16, 32, 2, 0, 0, 2>}},

@@ -526,7 +526,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const ConvSegment& cs = p.seg[0];
       const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
       const size_t src_bytes = (size_t)B * cs.H * cs.W * cs.ldc * esz;
-      if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand && cs.C == 128 &&
+      if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand &&
+          (cs.C == 128 || (cs.C == 256 && !res2)) &&
           cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && src_bytes < (1ull << 31) &&
           p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix &&
           (size_t)cs.H * cs.W * p.out_ldc * esz < (1ull << 31)) {
@@ -547,8 +548,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
         Packed& pk3 = packed[i];
         void*& wc = ni == 4 ? pk3.w_c3 : pk3.w_c3h;
         if (!wc) {
-          TV_HIP(hipMalloc(&wc, conv3x3_weight_bytes(p.ntiles, res)));
-          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, ni, wc, nullptr);
+          TV_HIP(hipMalloc(&wc, conv3x3_weight_bytes(p.ntiles, res, cs.C / 32)));
+          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, ni, cs.C / 32, wc, nullptr);
           if (rc) return rc;
           TV_HIP(hipDeviceSynchronize());
         }
@@ -716,7 +717,9 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     return launch_dwconvt_add(x, ws->B, src.H, src.W, src.C, (const float*)packed[i].w, op.up_s, a, ad.C, o, dst.H,
                               dst.W, op.sy, op.sx, dtype, s);
   }
-  if (ws->head_skip[i]) return TV_OK;  // fused into the 3x3 heads launch
+  if (ws->head_skip[i])  // fused into the 3x3 heads launch; an activation after the summed 1x1 runs here
+    return op.act == 2 ? launch_leaky_inplace(out, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad, s)
+                       : TV_OK;
   if (ws->head_fused[i]) {
     TV_HIP(hipMemsetAsync(out, 0, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad * sizeof(float), s));
     return launch_conv3x3(ws->params[i], ws->dparams + i, out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 1);
@@ -873,7 +876,7 @@ const char* Engine::op_kernel(int B, size_t i) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
-      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ">";
+      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";
     }

@@ -10,7 +10,9 @@
 //             out[2m + pi][2n + pj] = sum over the phase's (1 + pi) x (1 + pj) taps — exactly the
 //             transposed conv's 9 taps per 2x2 output block (no zero-stuffing, no wasted MACs),
 //             each written by the phase-scatter epilogue (up_s = 2, shift (pi, pj), no skip add)
-//        * Conv2d(F, k, 1) + LeakyReLU                        -> one GEMM into the fp32 output
+//        * Conv2d(F, k, 1) + LeakyReLU                        -> one GEMM into the fp32 output, or
+//          (fp16 / bf16) fused into the preceding 3x3 conv's epilogue: the F-channel activation
+//          at 4x resolution never reaches HBM
 #include "common.h"
 #include "planner.h"
 
@@ -102,7 +104,14 @@ int build_plan_protonet(const tv_model_desc& d, Plan* plan) {
   OpSpec o;
   o.kind = OP_CONV;
   o.label = "_output_layer + LeakyReLU -> fp32 NHWC";
-  o.segs = {SegSpec{x, "_output_layer", "", 0, F, 1, 1, 1, 0}};
+  o.segs = {SegSpec{x, "", "", 0, F, 1, 1, 1, 0}};
+  // as a one-head "block-diagonal" 1x1 so the engine can fuse it into the 3x3 conv's epilogue
+  // (conv3x3 EPI 1: MFMA on the rounded 3x3 output, fp32 partial sums of the 128-channel tiles
+  // added into the output, LeakyReLU applied by a pass over the k output channels afterwards)
+  o.stack_w = {"_output_layer"};
+  o.stack_n = {k};
+  o.diag_in_off = {0};
+  o.diag_out_off = {0};
   P.out_c = k;
   P.out_cpad = (k + 3) / 4 * 4;
   P.out_h = t.H;

@@ -16,9 +16,10 @@
 //               zero-area boxes drop the column: NaN <= thr is false);
 //   nms_compact one workgroup per image: order-preserving compaction of the kept columns.
 // assemble_mask: one workgroup per 1024 pixels of one image; the block's prototypes (any
-// strides: NCHW or the protonet's NHWC output) are staged in LDS as [k][pixel], each thread
-// forms 4 adjacent pixels of every detection and stores them as one 16-byte vector (the kernel
-// is HBM-write-bound: n x H x W x 4 bytes per image).
+// strides: NCHW or the protonet's NHWC output) are staged in LDS as [k][pixel] and the
+// detections' coefficient rows and box bounds in chunks of 64 (gathered through the NMS output
+// when given), each thread forms 4 adjacent pixels of every detection and stores them as one
+// 16-byte vector (the kernel is HBM-write-bound: n x H x W x 4 bytes per image).
 #include "common.h"
 
 #include <cstring>
@@ -182,12 +183,18 @@ struct MaskParams {
   const float* coeff;                // [B][n_max][K]
   const float* box;                  // [B][n_max][4] or null
   const int* counts;                 // [B] or null (= n_max)
+  const long long* det;              // [B][n_max] coefficient / box row per detection, or null (= d)
+  int rows;                          // coefficient / box rows per image (A when det, else n_max)
   int n_max;
   float* out;                        // [B][n_max][H][W]
 };
 
+constexpr int kMaskDets = 64;  // detections whose coefficients / box bounds are staged in LDS at once
+
 __global__ __launch_bounds__(kMaskThreads) void assemble_mask(const MaskParams p) {
-  extern __shared__ __attribute__((aligned(16))) float pr[];  // [K][kMaskPix]
+  extern __shared__ __attribute__((aligned(16))) float pr[];  // [K][kMaskPix], then the detection chunk
+  float* dc = pr + p.K * kMaskPix;                             // [kMaskDets][K] coefficients
+  float4* db4 = reinterpret_cast<float4*>(dc + kMaskDets * p.K);  // [kMaskDets] left, right, top, bottom
   const int b = blockIdx.y;
   const int n = p.counts ? min(p.counts[b], p.n_max) : p.n_max;
   if (n <= 0) return;
@@ -208,10 +215,8 @@ __global__ __launch_bounds__(kMaskThreads) void assemble_mask(const MaskParams p
     }
     pr[k * kMaskPix + q] = v;
   }
-  __syncthreads();
   const int q0 = 4 * threadIdx.x;
   const int pix = pix0 + q0;
-  if (pix >= hw) return;
   int yy[4], xx[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -219,40 +224,59 @@ __global__ __launch_bounds__(kMaskThreads) void assemble_mask(const MaskParams p
     xx[e] = (pix + e) - yy[e] * p.W;
   }
   const bool vec = (hw & 3) == 0;  // 16-byte stores: every row of a detection starts 16-byte aligned
-  const float* cb = p.coeff + (size_t)b * p.n_max * p.K;
-  const float* bb = p.box ? p.box + (size_t)b * p.n_max * 4 : nullptr;
+  const float* cb = p.coeff + (size_t)b * p.rows * p.K;
+  const float* bb = p.box ? p.box + (size_t)b * p.rows * 4 : nullptr;
+  const long long* db = p.det ? p.det + (size_t)b * p.n_max : nullptr;
   float* ob = p.out + (size_t)b * p.n_max * hw;
-  for (int d = 0; d < n; ++d) {
-    const float* c = cb + (size_t)d * p.K;
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < p.K; ++k) {
-      const float ck = c[k];
-      const float4 v = *reinterpret_cast<const float4*>(pr + k * kMaskPix + q0);
-      s[0] += ck * v.x;
-      s[1] += ck * v.y;
-      s[2] += ck * v.z;
-      s[3] += ck * v.w;
+  for (int d0 = 0; d0 < n; d0 += kMaskDets) {
+    const int nd = min(kMaskDets, n - d0);
+    __syncthreads();  // prototypes staged / the previous chunk consumed
+    // the chunk's coefficient rows (the NMS-kept anchors when det is given) and box bounds
+    for (int e = threadIdx.x; e < nd * p.K; e += kMaskThreads) {
+      const int d = e / p.K, k = e - d * p.K;
+      const size_t row = db ? (size_t)db[d0 + d] : (size_t)(d0 + d);
+      dc[e] = cb[row * p.K + k];
     }
-    float m[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) m[e] = 1.f / (1.f + expf(-s[e]));
-    if (bb) {
-      const float* q = bb + (size_t)d * 4;
-      const float by = q[0] * (float)p.H, bx = q[1] * (float)p.W, bh = q[2] * (float)p.H, bw = q[3] * (float)p.W;
-      const float left = bx - bw / 2, right = bx + bw / 2, top = by - bh / 2, bottom = by + bh / 2;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float fx = (float)xx[e], fy = (float)yy[e];
-        m[e] *= (fx >= left && fx <= right && fy >= top && fy <= bottom) ? 1.f : 0.f;
+    if (bb)
+      for (int d = threadIdx.x; d < nd; d += kMaskThreads) {
+        const size_t row = db ? (size_t)db[d0 + d] : (size_t)(d0 + d);
+        const float* q = bb + row * 4;
+        // box_to_mask (boxes.py:88-103): box scaled by (H, W, H, W), bounds as the reference forms them
+        const float by = q[0] * (float)p.H, bx = q[1] * (float)p.W, bh = q[2] * (float)p.H, bw = q[3] * (float)p.W;
+        db4[d] = make_float4(bx - bw / 2, bx + bw / 2, by - bh / 2, by + bh / 2);
       }
-    }
-    float* o = ob + (size_t)d * hw + pix;
-    if (vec) {
-      *reinterpret_cast<float4*>(o) = make_float4(m[0], m[1], m[2], m[3]);
-    } else {
+    __syncthreads();
+    if (pix >= hw) continue;
+    for (int d = 0; d < nd; ++d) {
+      const float* c = dc + d * p.K;
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int k = 0; k < p.K; ++k) {
+        const float ck = c[k];
+        const float4 v = *reinterpret_cast<const float4*>(pr + k * kMaskPix + q0);
+        s[0] += ck * v.x;
+        s[1] += ck * v.y;
+        s[2] += ck * v.z;
+        s[3] += ck * v.w;
+      }
+      float m[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (pix + e < hw) o[e] = m[e];
+      for (int e = 0; e < 4; ++e) m[e] = 1.f / (1.f + expf(-s[e]));
+      if (bb) {
+        const float4 bd = db4[d];  // left, right, top, bottom
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float fx = (float)xx[e], fy = (float)yy[e];
+          m[e] *= (fx >= bd.x && fx <= bd.y && fy >= bd.z && fy <= bd.w) ? 1.f : 0.f;
+        }
+      }
+      float* o = ob + (size_t)(d0 + d) * hw + pix;
+      if (vec) {
+        *reinterpret_cast<float4*>(o) = make_float4(m[0], m[1], m[2], m[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (pix + e < hw) o[e] = m[e];
+      }
     }
   }
 }
@@ -360,15 +384,15 @@ int launch_yolact_fast_nms(const float* cls, long long cls_bstride, int A, int C
 }
 
 int launch_yolact_assemble_mask(const float* proto, const long long pst[4], int B, int K, int H, int W,
-                                const float* coeff, const float* box, const int* counts, int n_max, float* out,
-                                hipStream_t s) {
+                                const float* coeff, const float* box, const int* counts, const long long* det,
+                                int rows, int n_max, float* out, hipStream_t s) {
   if (B < 1 || K < 1 || H < 1 || W < 1 || n_max < 0 || (long)H * W >= (1L << 30) || B > 65535) {
     set_error("assemble_mask: bad shapes");
     return 2;  // TV_ESHAPE
   }
   if (n_max == 0) return 0;
-  const size_t lds = (size_t)K * yolact::kMaskPix * sizeof(float);
-  if (lds > 160 * 1024) { set_error("assemble_mask: more than 40 prototypes"); return 2; }
+  const size_t lds = ((size_t)K * yolact::kMaskPix + (size_t)yolact::kMaskDets * (K + 4)) * sizeof(float);
+  if (lds > 160 * 1024) { set_error("assemble_mask: more than 37 prototypes"); return 2; }
   static std::once_flag attr_once;
   hipError_t attr_err = hipSuccess;
   std::call_once(attr_once, [&] {
@@ -376,7 +400,8 @@ int launch_yolact_assemble_mask(const float* proto, const long long pst[4], int 
                                    160 * 1024);
   });
   TV_HIP(attr_err);
-  yolact::MaskParams p{proto, pst[0], pst[1], pst[2], pst[3], K, H, W, coeff, box, counts, n_max, out};
+  yolact::MaskParams p{proto, pst[0], pst[1], pst[2], pst[3], K, H, W, coeff, box, counts, det, det ? rows : n_max,
+                       n_max, out};
   const int hw = H * W;
   hipLaunchKernelGGL(yolact::assemble_mask, dim3((hw + yolact::kMaskPix - 1) / yolact::kMaskPix, B),
                      dim3(yolact::kMaskThreads), lds, s, p);

@@ -63,6 +63,8 @@ EXPORTS = {
                                 c_i32),
     "tv_yolact_assemble_masks": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32,
                                   c_vp, c_vp], c_i32),
+    "tv_yolact_assemble_masks_indexed": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32,
+                                          c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
     "tv_last_error": ([], ctypes.c_char_p),
     "tv_version": ([], ctypes.c_char_p),
 }

@@ -247,3 +247,32 @@ def assemble_masks(mask_prototype: torch.Tensor, mask_coeff: torch.Tensor, box: 
                                                    ctypes.c_void_p(out.data_ptr()), _lib.stream_of(proto.device)),
                "assemble_masks")
     return out
+
+
+def assemble_masks_indexed(mask_prototype: torch.Tensor, mask_coeff: torch.Tensor, box: Optional[torch.Tensor],
+                           det: torch.Tensor, counts: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The node's mask step (yolact_node.py:134) for B images straight from BatchedNMS: prototypes
+    [B, K, H, W] (any strides), coefficients [B, A, K] and boxes [B, A, 4] (or None) of every anchor,
+    det [B, n] int64 / counts [B] int32 (BatchedNMS outputs) -> masks [B, n, H, W]; rows past
+    counts[b] are left untouched."""
+    proto = _proto_view(mask_prototype, "mask_prototype")
+    coeff = _f32(mask_coeff, "mask_coeff")
+    B, K, H, W = proto.shape
+    A = coeff.shape[1]
+    n = det.shape[1]
+    if coeff.shape != (B, A, K) or det.shape != (B, n) or det.dtype != torch.int64 or counts.shape != (B,) \
+            or counts.dtype != torch.int32:
+        raise ValueError("assemble_masks_indexed: need coeff [B, A, K], det [B, n] int64, counts [B] int32")
+    bptr = None
+    if box is not None:
+        box = _f32(box, "box")
+        if box.shape != (B, A, 4):
+            raise ValueError(f"assemble_masks_indexed: box {tuple(box.shape)} must be [{B}, {A}, 4]")
+        bptr = ctypes.c_void_p(box.data_ptr())
+    if out is None:
+        out = torch.empty((B, n, H, W), dtype=torch.float32, device=proto.device)
+    _lib.check(_lib.lib().tv_yolact_assemble_masks_indexed(
+        ctypes.c_void_p(proto.data_ptr()), _lib.strides(proto, 4), B, K, H, W, ctypes.c_void_p(coeff.data_ptr()), bptr,
+        A, ctypes.c_void_p(det.data_ptr()), ctypes.c_void_p(counts.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
+        _lib.stream_of(proto.device)), "assemble_masks_indexed")
+    return out

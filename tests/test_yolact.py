@@ -172,6 +172,18 @@ def test_gpu_large_and_degenerate_nms():
         ref = ry.nms(cls[b:b + 1], box[b:b + 1], 100, 0.5, 0.05).numpy()
         assert cnt[b] == len(ref)
         np.testing.assert_array_equal(det[b, :cnt[b]], ref)
+    # the node's mask step straight from the batched NMS output (yolact_node.py:134)
+    from tauv_vision_amd.yolact import assemble_mask, assemble_masks_indexed
+    gg = torch.Generator().manual_seed(11)
+    B, A = cls.shape[:2]
+    proto = torch.randn(B, 40, 44, 8, generator=gg).cuda().permute(0, 3, 1, 2)
+    coeff = torch.randn(B, A, 8, generator=gg).cuda()
+    bd, bc = bn(cls.cuda(), box.cuda(), 0.5, 0.05)
+    masks = assemble_masks_indexed(proto, coeff, box.cuda(), bd, bc).cpu()
+    for b in range(B):
+        d = torch.from_numpy(det[b, :cnt[b]]).cuda()
+        np.testing.assert_array_equal(masks[b, :cnt[b]].numpy(),
+                                      assemble_mask(proto[b], coeff[b, d], box.cuda()[b, d]).cpu().numpy())
 
 
 @pytest.mark.gpu
@@ -231,8 +243,11 @@ def test_gpu_protonet_matches_reference(name, precision):
         scale = float(np.abs(g["sample"]).max())
     record_measurement(f"protonet/{name}/{precision}", {"max_abs_err": err, "ref_absmax": scale})
     assert err <= PROTO_TOL[precision] * max(1.0, scale), f"{name} {precision}: {err}"
-    np.testing.assert_allclose(y.double().sum(dim=(0, 2, 3)).numpy(), g["chan_sum"],
-                               rtol=PROTO_TOL[precision] * 10)
+    # per-channel sums over every output (not just the sample): independent per-element errors
+    # grow like sqrt(n); a systematic bias would grow like n and fail this
+    npix = y.shape[0] * y.shape[2] * y.shape[3]
+    np.testing.assert_allclose(y.double().sum(dim=(0, 2, 3)).numpy(), g["chan_sum"], rtol=PROTO_TOL[precision],
+                               atol=4 * PROTO_TOL[precision] * max(1.0, scale) * npix ** 0.5)
 
 
 @pytest.mark.gpu

@@ -113,6 +113,15 @@ const char* tv_engine_op_kernel(tv_engine* engine, int32_t batch, int32_t index)
 #define TV_MAX_SLICES 8
 int tv_engine_slices(tv_engine* engine, int32_t batch, int32_t* n_slices, int32_t slice_batch[TV_MAX_SLICES]);
 
+/* The node's preprocessing of camera frames (centernet_node.py:90-92): T.ToTensor (u8 / 255) ->
+ * T.Resize((dst_h, dst_w)) (torchvision 0.15.2 tensor path: bilinear, align_corners=False, no
+ * antialias, evaluated as torch's CPU upsample_bilinear2d does) -> T.Normalize(ImageNet). u8 RGB
+ * frames NHWC [B, src_h, src_w, 3] -> normalised fp32 NCHW [B, 3, dst_h, dst_w], the input of
+ * tv_engine_forward. (Frames already at the model size take tv_engine_forward_u8 instead: the
+ * resize is then the identity and ToTensor + Normalize are fused into the stem.) */
+int tv_preprocess_u8(const uint8_t* frames, int32_t B, int32_t src_h, int32_t src_w, int32_t dst_h, int32_t dst_w,
+                     float* img_nchw, void* stream);
+
 /* heatmap_nms(sigmoid?(heat), k) (decode.py:239-252) over any strided [B,C,H,W] fp32
  * view; `out` is dense [B,C,H,W]. k must be odd and >= 1 (else TV_EINVAL, like the
  * reference's assert). */

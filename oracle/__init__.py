@@ -13,3 +13,4 @@ import it, and only as the checker / the timed CPU baseline. The product path
 from .ref_forward import centernet_forward, pad_to_match, head_channels_for, PredictionRef  # noqa: F401
 from .ref_decode import (heatmap_nms, heatmap_detect, decode, decode_keypoints,  # noqa: F401
                          depth_decode)
+from .ref_preprocess import preprocess  # noqa: F401

@@ -6,6 +6,9 @@
 //    skip tensor alone (dla.py:205-207 zero padding).
 #include "common.h"
 
+// expression order as the reference's torch ops (explicit __fmaf_rn where torch's CPU kernel fuses)
+#pragma clang fp contract(off)
+
 namespace tv {
 
 __constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
@@ -66,6 +69,59 @@ __global__ void prep_u8(const uint8_t* __restrict__ fr, int B, int H, int W, int
     for (int c = 0; c < 3; ++c) v[k][c] = ok ? ((float)row[xx * 3 + c] / 255.0f - kMean[c]) / kStd[c] : 0.0f;
   }
   write_expanded<T>(out + i * cpad, v, cpad);
+}
+
+// The node's preprocessing at camera resolution (centernet_node.py:90-92): ToTensor (u8 / 255),
+// torchvision 0.15.2 tensor Resize = F.interpolate(bilinear, align_corners=False, antialias=False)
+// as torch's CPU kernel evaluates it (upsample_bilinear2d: scale = in / out in fp32, source index
+// fma(scale, dst + 0.5, -0.5) clamped at 0, weights l1 = src - floor, l0 = 1 - l1, the row blend
+// fma(top, wh0, bottom * wh1) of the column blends fma(left, ww0, right * ww1)), then Normalize
+// ((v - mean) / std). One thread per output pixel; fp32 NCHW out (the Centernet.forward input).
+__device__ __forceinline__ void lin_index(int d, int in, float scale, int& i0, int& i1, float& l0, float& l1) {
+  float src = __fmaf_rn(scale, (float)d + 0.5f, -0.5f);
+  src = src < 0.f ? 0.f : src;
+  i0 = (int)src;
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+}
+
+__global__ void preprocess_u8(const uint8_t* __restrict__ fr, int B, int Hs, int Ws, int Ho, int Wo, float sh, float sw,
+                              float* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t hw = (size_t)Ho * Wo;
+  if (i >= (size_t)B * hw) return;
+  const int b = (int)(i / hw);
+  const int p = (int)(i - (size_t)b * hw);
+  const int y = p / Wo, x = p - (p / Wo) * Wo;
+  int h0, h1, w0, w1;
+  float a0, a1, b0, b1;
+  lin_index(y, Hs, sh, h0, h1, a0, a1);
+  lin_index(x, Ws, sw, w0, w1, b0, b1);
+  const uint8_t* f = fr + (size_t)b * Hs * Ws * 3;
+  const uint8_t* r0 = f + (size_t)h0 * Ws * 3;
+  const uint8_t* r1 = f + (size_t)h1 * Ws * 3;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float A = (float)r0[w0 * 3 + c] / 255.0f, Bv = (float)r0[w1 * 3 + c] / 255.0f;
+    const float C = (float)r1[w0 * 3 + c] / 255.0f, D = (float)r1[w1 * 3 + c] / 255.0f;
+    const float t0 = __fmaf_rn(A, b0, Bv * b1);
+    const float t1 = __fmaf_rn(C, b0, D * b1);
+    const float v = __fmaf_rn(t0, a0, t1 * a1);
+    out[((size_t)b * 3 + c) * hw + p] = (v - kMean[c]) / kStd[c];
+  }
+}
+
+int launch_preprocess_u8(const uint8_t* frames, int B, int Hs, int Ws, int Ho, int Wo, float* out, hipStream_t s) {
+  if (B < 1 || Hs < 1 || Ws < 1 || Ho < 1 || Wo < 1 || (long)B * Ho * Wo >= (1L << 31)) {
+    set_error("preprocess: bad shapes");
+    return 1;
+  }
+  const size_t n = (size_t)B * Ho * Wo;
+  hipLaunchKernelGGL(preprocess_u8, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, frames, B, Hs, Ws, Ho, Wo,
+                     (float)Hs / (float)Ho, (float)Ws / (float)Wo, out);
+  TV_HIP(hipGetLastError());
+  return 0;
 }
 
 template <typename F>

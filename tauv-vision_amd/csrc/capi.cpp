@@ -161,6 +161,14 @@ const char* tv_engine_op_kernel(tv_engine* e, int32_t B, int32_t i) {
   return e->e.op_kernel(B, i);
 }
 
+int tv_preprocess_u8(const uint8_t* frames, int32_t B, int32_t src_h, int32_t src_w, int32_t dst_h, int32_t dst_w,
+                     float* img_nchw, void* stream) {
+  TV_GUARD({
+    if (!frames || !img_nchw) { set_error("null argument"); return TV_EINVAL; }
+    return launch_preprocess_u8(frames, B, src_h, src_w, dst_h, dst_w, img_nchw, (hipStream_t)stream);
+  })
+}
+
 int tv_heatmap_nms(const float* heat, const int64_t st[4], int32_t B, int32_t C, int32_t H, int32_t W, int32_t k,
                    int32_t apply_sigmoid, float* out, void* stream) {
   TV_GUARD({

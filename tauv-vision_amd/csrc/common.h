@@ -148,6 +148,9 @@ int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad,
                      hipStream_t s);
 int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cpad, int dtype,
                    hipStream_t s);
+// ToTensor + bilinear Resize (torchvision 0.15.2 tensor semantics) + Normalize of u8 HWC frames at
+// camera resolution -> normalised fp32 NCHW [B, 3, Ho, Wo] (centernet_node.py:90-92)
+int launch_preprocess_u8(const uint8_t* frames, int B, int Hs, int Ws, int Ho, int Wo, float* out, hipStream_t s);
 // leaky_relu(0.01) in place over n fp32 values (n % 4 == 0)
 int launch_leaky_inplace(float* x, size_t n, hipStream_t s);
 // fp32 NCHW [B, C, H, W] -> NHWC compute dtype with pixel stride ldc (protonet input)

@@ -46,6 +46,7 @@ EXPORTS = {
     "tv_engine_op_label": ([c_vp, c_i32], ctypes.c_char_p),
     "tv_engine_op_kernel": ([c_vp, c_i32, c_i32], ctypes.c_char_p),
     "tv_engine_slices": ([c_vp, c_i32, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)], c_i32),
+    "tv_preprocess_u8": ([c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp], c_i32),
     "tv_heatmap_nms": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp], c_i32),
     "tv_heatmap_topk": ([c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp], c_i32),
     "tv_index_split": ([c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp], c_i32),

@@ -7,6 +7,7 @@ forward pass is one native call (all convolutions as fused MFMA implicit GEMMs, 
 csrc/planner.cpp) and returns the reference's `Prediction`, whose tensors are channel
 slices of one fp32 NHWC head tensor (same shapes and values, different strides).
 """
+import ctypes
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -143,22 +144,30 @@ class _NativeModel(nn.Module):
         eng = self.engine(dev, img.shape[2], img.shape[3])
         return prediction_from_nhwc(eng.forward(img), self.object_config)
 
-    def forward_frames(self, frames: torch.Tensor) -> Prediction:
-        """Raw uint8 RGB frames [B, H, W, 3] (or [H, W, 3]) with the node's ToTensor +
-        ImageNet Normalize (centernet_node.py:90-92) fused into the first kernel."""
+    def forward_frames(self, frames: torch.Tensor, size=None) -> Prediction:
+        """Raw uint8 RGB camera frames [B, H, W, 3] (or [H, W, 3]) through the node's
+        preprocessing (centernet_node.py:90-92): ToTensor -> Resize(size) -> Normalize(ImageNet).
+        size = (in_h, in_w) of the model (None: the frames' own size). At the model size the
+        resize is the identity and ToTensor + Normalize are fused into the stem kernel; otherwise
+        one kernel resizes + normalises (tv_preprocess_u8) into the fp32 forward() input."""
         if frames.dim() == 3:
             frames = frames.unsqueeze(0)
         if frames.dtype != torch.uint8 or frames.shape[-1] != 3:
             raise ValueError("frames must be uint8 [B, H, W, 3]")
         dev = self._device_for(frames)
         frames = frames.to(dev).contiguous()
-        eng = self.engine(dev, frames.shape[1], frames.shape[2])
-        return prediction_from_nhwc(eng.forward_u8(frames), self.object_config)
+        in_h, in_w = (frames.shape[1], frames.shape[2]) if size is None else (int(size[0]), int(size[1]))
+        eng = self.engine(dev, in_h, in_w)
+        if (in_h, in_w) == (frames.shape[1], frames.shape[2]):
+            return prediction_from_nhwc(eng.forward_u8(frames), self.object_config)
+        return prediction_from_nhwc(eng.forward(preprocess(frames, in_h, in_w)), self.object_config)
 
     def detect(self, frames: torch.Tensor, model_config, n_detections: int = 100, score_threshold: float = 0.3):
-        """detect(frames) == decode(forward(preprocess(frames)), ...)."""
+        """detect(frames) == decode(forward(preprocess(frames)), ...): camera frames of any size,
+        resized to (model_config.in_h, model_config.in_w) like the node."""
         from .decode import decode
-        return decode(self.forward_frames(frames), model_config, n_detections, score_threshold)
+        return decode(self.forward_frames(frames, (model_config.in_h, model_config.in_w)), model_config,
+                      n_detections, score_threshold)
 
 
 class Centernet(_NativeModel):
@@ -199,6 +208,26 @@ class CenterpointDLA34(_NativeModel):
 
     def _desc(self, in_h, in_w):
         return dla34_desc(self.head_channels, in_h, in_w, self.precision)
+
+
+def preprocess(frames: torch.Tensor, in_h: int, in_w: int) -> torch.Tensor:
+    """The node's T.ToTensor -> T.Resize((in_h, in_w)) -> T.Normalize(ImageNet)
+    (centernet_node.py:90-92) on the GPU: u8 RGB frames [B, H, W, 3] (or [H, W, 3]) at camera
+    resolution -> normalised fp32 [B, 3, in_h, in_w] (bilinear, align_corners=False, no antialias:
+    torchvision 0.15.2's tensor Resize)."""
+    if frames.dim() == 3:
+        frames = frames.unsqueeze(0)
+    if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[-1] != 3:
+        raise ValueError("frames must be uint8 [B, H, W, 3]")
+    if not torch.cuda.is_available():
+        raise RuntimeError("tauv_vision_amd needs a gfx950 (MI355X) GPU; no HIP device is visible")
+    frames = (frames if frames.is_cuda else frames.cuda()).contiguous()
+    B, H, W, _ = frames.shape
+    out = torch.empty((B, 3, int(in_h), int(in_w)), dtype=torch.float32, device=frames.device)
+    _lib.check(_lib.lib().tv_preprocess_u8(ctypes.c_void_p(frames.data_ptr()), B, H, W, int(in_h), int(in_w),
+                                           ctypes.c_void_p(out.data_ptr()), _lib.stream_of(frames.device)),
+               "preprocess")
+    return out
 
 
 def initialize_weights(module: nn.Module, excluded_modules=()):

@@ -89,8 +89,15 @@ int tv_model_geometry(const tv_model_desc* desc, double* flops_per_frame, int32_
 int tv_engine_create(const tv_model_desc* desc, const tv_weight_view* weights, int32_t n_weights,
                      int32_t device, tv_engine** out);
 int tv_engine_destroy(tv_engine* engine);
+/* Workspaces: the first forward of a batch size on a stream allocates that (stream, batch)
+ * pair's activation arena (hipMalloc: not inside a graph capture) and keeps it for later calls;
+ * a caller that cycles through many batch sizes or streams bounds the device memory with
+ * tv_engine_trim. */
 /* Allocate the per-(stream, batch) workspace up front (required before graph capture). */
 int tv_engine_prepare(tv_engine* engine, int32_t batch, void* stream);
+/* Free every cached workspace (synchronises the device; no forward on this engine may be in
+ * flight or concurrent, and graphs captured over the freed arenas must not be replayed). */
+int tv_engine_trim(tv_engine* engine);
 /* Centernet.forward(img) -> Prediction heads (centernet.py:65-92). Async on `stream`. */
 int tv_engine_forward(tv_engine* engine, const float* img_nchw, int32_t batch, float* out_nhwc, void* stream);
 /* Same from raw u8 RGB frames with ToTensor + Normalize fused (centernet_node.py:90-92). */

@@ -105,6 +105,13 @@ int tv_engine_prepare(tv_engine* e, int32_t B, void* stream) {
   })
 }
 
+int tv_engine_trim(tv_engine* e) {
+  TV_GUARD({
+    if (!e) { set_error("null engine"); return TV_EINVAL; }
+    return e->e.trim();
+  })
+}
+
 int tv_engine_forward(tv_engine* e, const float* img, int32_t B, float* out, void* stream) {
   TV_GUARD({
     if (!e) { set_error("null engine"); return TV_EINVAL; }

@@ -674,6 +674,20 @@ int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
   return TV_OK;
 }
 
+int Engine::trim() {
+  std::lock_guard<std::mutex> g(mu);
+  TV_HIP(hipSetDevice(device));
+  TV_HIP(hipDeviceSynchronize());  // no queued launch still reads an arena
+  for (auto& kv : workspaces) {
+    if (kv.second->arena) (void)hipFree(kv.second->arena);
+    if (kv.second->dparams) (void)hipFree(kv.second->dparams);
+    if (kv.second->dks) (void)hipFree(kv.second->dks);
+    delete kv.second;
+  }
+  workspaces.clear();
+  return TV_OK;
+}
+
 int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, float* out, hipStream_t s) {
   const OpSpec& op = plan.ops[i];
   char* base = (char*)ws->arena;

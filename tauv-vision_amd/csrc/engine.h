@@ -91,6 +91,7 @@ struct Engine {
   int create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev);
   int get_workspace(int B, hipStream_t s, Workspace** out);
   int prepare(int B, hipStream_t s);  // workspaces (and side stream) for forward(B) on s
+  int trim();                         // free every cached workspace (no forward may be in flight)
   int forward(const void* input, int input_u8, int B, float* out, hipStream_t s);
   int profile(const void* input, int input_u8, int B, float* out, hipStream_t s, float* ms, double* flops, int cap, int* n_ops);
   const char* op_kernel(int B, size_t i);

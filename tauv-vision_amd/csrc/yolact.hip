@@ -87,7 +87,11 @@ __global__ __launch_bounds__(256) void nms_keys(const float* __restrict__ cls, l
   float s = 0.f;
   for (int j = 0; j < C1; ++j) s += expf(c[j] - m);
   float best = 0.f;
-  for (int j = 1; j < C1; ++j) best = fmaxf(best, expf(c[j] - m) / s);
+  for (int j = 1; j < C1; ++j) {
+    const float v = expf(c[j] - m) / s;
+    best = (v > best || v != v) ? v : best;  // torch.max propagates a NaN softmax (NaN logits)
+  }
+  // a NaN confidence sorts first (torch.sort, descending) and fails conf >= thr, like the reference
   keys[i] = order_bits(best);
 }
 

@@ -37,6 +37,7 @@ EXPORTS = {
                           ctypes.POINTER(c_vp)], c_i32),
     "tv_engine_destroy": ([c_vp], c_i32),
     "tv_engine_prepare": ([c_vp, c_i32, c_vp], c_i32),
+    "tv_engine_trim": ([c_vp], c_i32),
     "tv_engine_forward": ([c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
     "tv_engine_forward_u8": ([c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
     "tv_engine_profile": ([c_vp, c_vp, c_i32, c_vp, c_vp, ctypes.POINTER(c_f32), ctypes.POINTER(c_f64), c_i32,

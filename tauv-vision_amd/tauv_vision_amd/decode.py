@@ -3,9 +3,13 @@ native gfx950 kernels: sigmoid + 3x3 peak NMS, exact per-image top-K and the per
 gather run on the GPU (csrc/decode.hip) and return one packed record buffer, copied to the
 host once — instead of one device sync per scalar (decode.py:211-221).
 
-Differences from the reference, all value-preserving:
+Differences from the reference:
   * Detection.label / .score are 0-d CPU tensors (the reference's are 0-d tensors on the
     prediction's device, decode.py:212-213); y/x/h/w/depth are Python floats.
+  * decode()'s y / x: the reference forms (R * i + offset) / in_h in float64 Python arithmetic
+    (decode.py:214-215); the kernel evaluates the same expression in double but the record
+    stores it as fp32, so y / x are that float64 value rounded to fp32 (relative error
+    <= 6e-8). h / w / depth / score are the reference's fp32 values exactly.
   * top-K ties are broken toward the smaller flat index (torch.topk: unspecified).
   * label / y / x use integer division (== the reference's float32 division, decode.py:271-277,
     while C*H*W < 2^24).

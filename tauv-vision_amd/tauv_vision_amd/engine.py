@@ -56,6 +56,10 @@ class NativeEngine:
     def prepare(self, batch):
         _lib.check(_lib.lib().tv_engine_prepare(self._h, int(batch), _lib.stream_of(self.device)), "prepare")
 
+    def trim(self):
+        """Free every cached (stream, batch) workspace (synchronises the device)."""
+        _lib.check(_lib.lib().tv_engine_trim(self._h), "trim")
+
     def forward(self, img, out=None):
         """img: fp32 NCHW on this device; returns the fp32 NHWC head tensor."""
         B = img.shape[0]

@@ -238,3 +238,16 @@ def test_kernel_selection_full_size(precision):
     assert kern["heads.*.2 (block-diagonal) -> fp32 NHWC"] == "(fused into the 3x3 heads)"
     assert kern["backbone.ida_up_reverse.upsample_layers.0+pad_to_match+add"].startswith("tv::convt::convt_add<")
     assert kern["backbone.multi_ida_up.ida_up_layers.0.output_layers.0.0"].startswith("tv::c3::conv3x3<")
+
+
+def test_engine_trim_frees_and_rebuilds_workspaces():
+    """tv_engine_trim drops every cached (stream, batch) arena; later forwards rebuild them and
+    give the same results."""
+    model, oc, mc, case = build("r18_c16_b2_96x128", "fp16")
+    img = case_input("r18_c16_b2_96x128").cuda()
+    eng = model.engine(img.device, case["in_h"], case["in_w"])
+    before = [eng.forward(img[:b]).clone() for b in (1, 2)]
+    eng.trim()
+    after = [eng.forward(img[:b]) for b in (1, 2)]
+    for a, b in zip(before, after):
+        assert torch.equal(a, b)

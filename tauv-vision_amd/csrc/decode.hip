@@ -74,6 +74,8 @@ constexpr int kMergeThreads = 1024;
 constexpr int kMergePer = 16;
 constexpr int kMergeCap = kMergeThreads * kMergePer;     // 16384 candidates per merge workgroup
 constexpr int kMaxK = 1024;
+constexpr int kSmallMergeThreads = 256, kSmallMergePer = 4;
+constexpr int kSmallMergeCap = kSmallMergeThreads * kSmallMergePer;
 
 __device__ __forceinline__ uint32_t order_bits(float f) {
   uint32_t u = __float_as_uint(f);
@@ -251,28 +253,41 @@ __global__ __launch_bounds__(kTileThreads) void tile_select(const float* __restr
   const int LH = nh + 2 * r, LW = nw + 2 * r;
   const float* base = heat + b * s0;
 
-  // tile + halo -> LDS [cc][yy][xx], sigmoid applied once per element; outside the image -inf
+  // tile + halo -> LDS [cc][yy][xx], sigmoid applied once per element; outside the image -inf.
+  // Loads are issued in batches of kFillBatch per thread before any is consumed, so a block pays
+  // one memory latency per batch instead of one per element.
   const int nl = nc * LH * LW;
-  for (int e = threadIdx.x; e < nl; e += kTileThreads) {
-    int cc, yy, xx;
-    if (g.chan_fast) {
-      cc = e % nc;
-      const int p = e / nc;
-      xx = p % LW;
-      yy = p / LW;
-    } else {
-      xx = e % LW;
-      const int p = e / LW;
-      yy = p % LH;
-      cc = p / LH;
+  constexpr int kFillBatch = 8;
+  for (int e0 = 0; e0 < nl; e0 += kTileThreads * kFillBatch) {
+    float v[kFillBatch];
+    int dst[kFillBatch];
+    bool inb[kFillBatch];
+#pragma unroll
+    for (int j = 0; j < kFillBatch; ++j) {
+      const int e = e0 + j * kTileThreads + threadIdx.x;
+      int cc, yy, xx;
+      if (g.chan_fast) {
+        cc = e % nc;
+        const int p = e / nc;
+        xx = p % LW;
+        yy = p / LW;
+      } else {
+        xx = e % LW;
+        const int p = e / LW;
+        yy = p % LH;
+        cc = p / LH;
+      }
+      const int y = y0 + yy - r, x = x0 + xx - r;
+      const bool in = e < nl && y >= 0 && y < H && x >= 0 && x < W;
+      inb[j] = in;
+      v[j] = in ? base[(int64_t)(c0 + cc) * s1 + (int64_t)y * s2 + (int64_t)x * s3] : 0.f;
+      dst[j] = e < nl ? (cc * LH + yy) * LW + xx : -1;
     }
-    const int y = y0 + yy - r, x = x0 + xx - r;
-    float v = -INFINITY;
-    if (y >= 0 && y < H && x >= 0 && x < W) {
-      v = base[(int64_t)(c0 + cc) * s1 + (int64_t)y * s2 + (int64_t)x * s3];
-      if (g.apply_sigmoid) v = sigmoidf_ref(v);
+#pragma unroll
+    for (int j = 0; j < kFillBatch; ++j) {
+      if (dst[j] < 0) continue;
+      tile[dst[j]] = !inb[j] ? -INFINITY : g.apply_sigmoid ? sigmoidf_ref(v[j]) : v[j];
     }
-    tile[(cc * LH + yy) * LW + xx] = v;
   }
   __syncthreads();
 
@@ -315,10 +330,11 @@ __global__ __launch_bounds__(kTileThreads) void tile_select(const float* __restr
 }
 
 // ---- stage 2: merge candidate lists (K slots each) -> top K -----------------------------
+template <int NT>
 __device__ void bitonic_desc(uint64_t* a, int P) {
   for (int k = 2; k <= P; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < P; i += kMergeThreads) {
+      for (int i = threadIdx.x; i < P; i += NT) {
         const int ixj = i ^ j;
         if (ixj > i) {
           const uint64_t x = a[i], y = a[ixj];
@@ -340,9 +356,13 @@ struct MergeOut {
   int records;         // 1: also write detection records (DecodeParams)
 };
 
-__global__ __launch_bounds__(kMergeThreads) void merge_select(const uint64_t* __restrict__ in, int lists, int group,
-                                                              int K, uint64_t* __restrict__ next, int final_level,
-                                                              const MergeOut mo, const DecodeParams p) {
+// NT x PER candidate slots per workgroup: the full-size variant (1024 x 16) for the intermediate
+// levels, a 256 x 4 one when a single workgroup's candidates fit (B x 10 lists of K = 100 at
+// 120x160): a quarter of the waves in every block-wide step
+template <int NT, int PER>
+__global__ __launch_bounds__(NT) void merge_select(const uint64_t* __restrict__ in, int lists, int group, int K,
+                                                   uint64_t* __restrict__ next, int final_level, const MergeOut mo,
+                                                   const DecodeParams p) {
   __shared__ SelectShared sh;
   __shared__ uint64_t top[kMaxK];
   __shared__ int cnt_thr;
@@ -350,39 +370,39 @@ __global__ __launch_bounds__(kMergeThreads) void merge_select(const uint64_t* __
   const int l0 = grp * group, nl = min(group, lists - l0);
   const uint64_t* src = in + ((size_t)b * lists + l0) * K;
   const int n = nl * K;
-  uint64_t k[kMergePer];
+  uint64_t k[PER];
   int local = 0;
 #pragma unroll
-  for (int j = 0; j < kMergePer; ++j) {
-    const int e = threadIdx.x + j * kMergeThreads;
+  for (int j = 0; j < PER; ++j) {
+    const int e = threadIdx.x + j * NT;
     k[j] = e < n ? src[e] : 0;
     local += k[j] != 0;
   }
-  const int real = block_count_real<kMergeThreads>(local, sh);
+  const int real = block_count_real<NT>(local, sh);
   const int kt = min(K, real);
-  const uint64_t T = block_select<kMergeThreads, kMergePer>(k, kt, sh);
+  const uint64_t T = block_select<NT, PER>(k, kt, sh);
   if (threadIdx.x == 0) { sh.nout = 0; cnt_thr = 0; }
   __syncthreads();
   if (!final_level) {
     uint64_t* out = next + ((size_t)b * gridDim.x + grp) * K;
 #pragma unroll
-    for (int j = 0; j < kMergePer; ++j)
+    for (int j = 0; j < PER; ++j)
       if (k[j] != 0 && k[j] >= T) out[atomicAdd(&sh.nout, 1)] = k[j];
     __syncthreads();
-    for (int i = sh.nout + threadIdx.x; i < K; i += kMergeThreads) out[i] = 0;
+    for (int i = sh.nout + threadIdx.x; i < K; i += NT) out[i] = 0;
     return;
   }
 #pragma unroll
-  for (int j = 0; j < kMergePer; ++j)
+  for (int j = 0; j < PER; ++j)
     if (k[j] != 0 && k[j] >= T) top[atomicAdd(&sh.nout, 1)] = k[j];
   int P = 1;
   while (P < K) P <<= 1;
   __syncthreads();
-  for (int i = sh.nout + threadIdx.x; i < P; i += kMergeThreads) top[i] = 0;
+  for (int i = sh.nout + threadIdx.x; i < P; i += NT) top[i] = 0;
   __syncthreads();
-  bitonic_desc(top, P);
+  bitonic_desc<NT>(top, P);
   int local_thr = 0;
-  for (int i = threadIdx.x; i < K; i += kMergeThreads) {
+  for (int i = threadIdx.x; i < K; i += NT) {
     const uint64_t key = top[i];
     const float score = unorder_bits((uint32_t)(key >> 32));
     const int idx = (int)(0xFFFFFFFFu - (uint32_t)key);
@@ -503,7 +523,12 @@ int launch_select(const float* heat, const int64_t st[4], int B, int C, int H, i
     const int fin = groups == 1;
     uint64_t* in = buf[i & 1];
     uint64_t* nxt = buf[(i + 1) & 1];
-    hipLaunchKernelGGL(merge_select, dim3(groups, B), dim3(kMergeThreads), 0, s, in, lists, group, K, nxt, fin, mo, p);
+    if (fin && lists * K <= kSmallMergeCap)
+      hipLaunchKernelGGL((merge_select<kSmallMergeThreads, kSmallMergePer>), dim3(groups, B), dim3(kSmallMergeThreads), 0,
+                         s, in, lists, group, K, nxt, fin, mo, p);
+    else
+      hipLaunchKernelGGL((merge_select<kMergeThreads, kMergePer>), dim3(groups, B), dim3(kMergeThreads), 0, s, in, lists,
+                         group, K, nxt, fin, mo, p);
     TV_HIP(hipGetLastError());
     if (fin) break;
   }

@@ -71,15 +71,27 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int phase0 = group * NP;
 
   // ---- the group's weights and bias into LDS (rows n = phase*C + co of the packed [N][Kpad])
+  // (every load of the copy is issued before the first LDS write: one memory latency for the whole
+  // prologue instead of one per 16-byte chunk, which serialised ~16 L2/HBM round trips per wave)
   {
     const char* wsrc = reinterpret_cast<const char*>(p.weight) + (size_t)phase0 * C * p.Kpad * sizeof(T);
-    for (int i = tid; i < NP * C * 16; i += NT) {
+    constexpr int NCH = NP * C * 16 / NT;  // 16-byte chunks per thread (NP * 4)
+    static_assert((NP * C * 16) % NT == 0 && NP * C <= NT, "prologue split");
+    uint4 wv[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int i = tid + k * NT;
       const int r = i >> 4, c = i & 15;  // r = phase-in-group * C + co
-      *reinterpret_cast<uint4*>(smem + r * WPITCH + c * 16) =
-          *reinterpret_cast<const uint4*>(wsrc + (size_t)r * p.Kpad * sizeof(T) + c * 16);
+      wv[k] = *reinterpret_cast<const uint4*>(wsrc + (size_t)r * p.Kpad * sizeof(T) + c * 16);
     }
     float* lb = reinterpret_cast<float*>(smem + NP * PW);
-    for (int i = tid; i < NP * C; i += NT) lb[i] = p.bias[phase0 * C + i];
+    const float bv = tid < NP * C ? p.bias[phase0 * C + tid] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int i = tid + k * NT;
+      *reinterpret_cast<uint4*>(smem + (i >> 4) * WPITCH + (i & 15) * 16) = wv[k];
+    }
+    if (tid < NP * C) lb[tid] = bv;
   }
   __syncthreads();
 

@@ -56,7 +56,8 @@ struct Engine {
   void* zero_page = nullptr;   // 256 zero bytes: padding source for LDS-DMA
   int pipe_mode = 1;           // -1 auto (>= 256 tiles), 0 never, 1 whenever representable (env TV_CONV_PIPE)
   int c3_tw_force = 0;         // conv3x3 tile width override (env TV_C3_TW = 16 / 32)
-  int s2_min_tiles = -1;       // stride-2 halo kernel from this many tiles (env TV_S2_MINTILES; -1 = cu_count)
+  int s2_min_tiles = 1;        // stride-2 halo kernel from this many tiles (env TV_S2_MINTILES; -1 = cu_count; measured:
+                               // at B=1 the halo kernel beats the implicit GEMM on the small levels too)
   int c3_ni_force = 0;         // conv3x3 channel tile: 0 = by grid rounds, 2 / 4 forced (env TV_C3_NI)
   int c3_half_cost = 55;       // cost of a 64-channel half tile in % of a full one (env TV_C3_HALF_COST, 0 = never)
   int conv3_min_pix = 1;       // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)

@@ -87,7 +87,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   {
     const uint4* ws = reinterpret_cast<const uint4*>(p.weight);
     uint4* wd = reinterpret_cast<uint4*>(smem + OFF_W);
-    for (int i = tid; i < WF_BYTES / 16; i += NT) wd[i] = ws[i];
+    // all loads issued before the LDS writes (one memory latency, not one per chunk)
+    constexpr int NCH = (WF_BYTES / 16 + NT - 1) / NT;
+    uint4 wv[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) wv[k] = tid + k * NT < WF_BYTES / 16 ? ws[tid + k * NT] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+      if (tid + k * NT < WF_BYTES / 16) wd[tid + k * NT] = wv[k];
     float* lb = reinterpret_cast<float*>(smem + OFF_B);
     if (tid < 128) lb[tid] = tid < p.N ? p.bias[tid] : 0.0f;
     if constexpr (U8) {

@@ -83,3 +83,82 @@ def test_shard_bounds():
     assert shard_bounds(64, 0, 1) == (0, 64)
     with pytest.raises(ValueError):
         shard_bounds(4, 2, 2)
+
+
+# ---- end to end: per-rank forward + decode of a frame shard -> RecordGather -> detections ----
+E2E = dict(heights=[2] * 5, channels=[16] * 6, ds=2, H=96, W=128, K=20, thr=0.05, n=5)
+
+
+def _e2e_frames():
+    from recipe import seeded_u8_frames, normalize
+    fr = seeded_u8_frames(E2E["n"], E2E["H"], E2E["W"], seed=21)
+    return normalize(fr.permute(0, 3, 1, 2).float() / 255.0)
+
+
+def _e2e_sd():
+    import oracle
+    from recipe import seeded_state_dict
+    from tauv_vision_amd.weights import model_desc, param_layout
+    desc = model_desc(E2E["heights"], E2E["channels"], E2E["ds"], [4, 2, 2])
+    return seeded_state_dict(param_layout(desc)), oracle
+
+
+def _pack(dets, K):
+    """One frame's decode() output in the device record layout [K, 10] + count (decode.hip
+    merge_select: label, score, y, x, h, w, depth, flat index, aux0, aux1)."""
+    r = np.zeros((K, REC), np.float32)
+    for i, (lab, sc, y, x, h, w, d) in enumerate(dets):
+        r[i, :7] = (lab, sc, y, x, h, w, np.nan if d is None else d)
+    return r, len(dets)
+
+
+def e2e_worker(rank, world, port, q):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sd, oracle = _e2e_sd()
+        img = _e2e_frames()
+        n, K = E2E["n"], E2E["K"]
+        lo, hi = shard_bounds(n, rank, world)
+        per = -(-n // world)
+        rec = torch.zeros((per, K, REC))
+        cnt = torch.zeros((per,), dtype=torch.int32)  # short shard: padded frames with 0 records
+        if hi > lo:
+            with torch.no_grad():
+                pred = oracle.centernet_forward(sd, img[lo:hi], E2E["heights"], E2E["ds"], {})
+            for i, dets in enumerate(oracle.decode(pred, E2E["H"], E2E["W"], E2E["ds"], K, E2E["thr"])):
+                r, c = _pack(dets, K)
+                rec[i], cnt[i] = torch.from_numpy(r), c
+        all_rec, all_cnt = RecordGather(per, K, "cpu")(rec, cnt)
+        if rank == 0:
+            q.put((all_rec[:n].numpy().copy(), all_cnt[:n].numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_sharded_forward_decode_gather_matches_single_process():
+    """Frames sharded over 2 gloo ranks (5 frames: shards of 3 and 2), each rank runs forward +
+    decode on its own frames, one all-gather of the fixed-size records, host conversion — equals
+    decode() of the whole batch in one process (frames are independent)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=e2e_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    rec, cnt = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sd, oracle = _e2e_sd()
+    with torch.no_grad():
+        pred = oracle.centernet_forward(sd, _e2e_frames(), E2E["heights"], E2E["ds"], {})
+    want = oracle.decode(pred, E2E["H"], E2E["W"], E2E["ds"], E2E["K"], E2E["thr"])
+    got = records_to_detections(rec, cnt, has_depth=False)
+    assert [len(g) for g in got] == [len(w) for w in want]
+    for gb, wb in zip(got, want):
+        for d, w in zip(gb, wb):
+            assert int(d.label) == w[0]
+            assert float(d.score) == np.float32(w[1])
+            assert d.y == float(np.float32(w[2])) and d.x == float(np.float32(w[3]))
+            assert d.h == w[4] and d.w == w[5]

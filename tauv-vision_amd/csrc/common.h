@@ -75,7 +75,7 @@ struct ConvParams {
   const void* head_w;   // [ntiles][8 k-steps][64 lanes][16 B] MFMA A-fragments of the 1x1 weights
   const float* head_b;  // [ntiles][32] 1x1 bias on the first tile of each head, zeros elsewhere
   int head_ldc;
-  int head_row0[8], head_nrows[8];
+  int head_row0[16], head_nrows[16];
 };
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
@@ -87,7 +87,7 @@ constexpr int kPipeTileM = 256;
 // input (seg[0].C): 512-pixel
 // tiles of tw (16 or 32) columns; ConvParams.mtiles = conv3x3_tiles(B, H, W, tw); `grid`
 // persistent workgroups (one per CU, a multiple of 8 when >= 8).
-constexpr int kConv3MaxN = 1024;
+constexpr int kConv3MaxN = 2048;
 // epi = 0: store the activations; epi = 1: fused 1x1 heads into the fp32 output `out` (head_*)
 // res = 1: two segments — seg 0 the 3x3 input, seg 1 a 1x1 conv (stride seg[1].stride) over a
 // 128-channel tensor summed into the same accumulators (ResidualBlock conv2 + conv_residual)

@@ -1,631 +1,9 @@
-// Persistent halo-tile 3x3 / stride 1 / pad 1 convolution (gfx950, fp16 / bf16) — the
-// dominant shape of the DLA backbone at 120x160 (IDA projection/output convs, tree conv1s,
-// the stacked heads), reference dla.py ResidualBlock/IDAUp convs and centernet.py heads.
-//
-// Why not the implicit GEMM (conv_pipe.hip) for these: per 256-pixel tile the implicit GEMM
-// moves each input pixel 9 times (once per tap) and the 295 KB weight panel once, ~880 KB of
-// L2 -> LDS traffic per 75 MFLOP; measured, its main loop ran at ~21 B/clk/CU of LDS-DMA and
-// its per-tile prologue (first ring stages from L2/HBM) and LDS-staged epilogue were exposed
-// (tools/stamps.py: 13.5k + 41k + 9k cycles per tile against 18k of MFMA work).
-//
-// Design:
-//  * one 512-thread workgroup per CU (8 waves, two per SIMD), persistent over a static list of
-//    (spatial tile, 128-channel tile) pairs, XCD-aware: each XCD owns a contiguous tile range so
-//    neighbouring tiles (shared halo rows) meet in its L2. Two waves per SIMD because an
-//    LDS-DMA instruction stalls its wave for ~60-180 cycles at issue: with one wave per SIMD
-//    that stall idles the matrix core (measured: 1550 instead of 1024 cycles per k-step);
-//  * a tile = TH x TW = 512 output pixels of one frame x 128 output channels; each wave owns
-//    64 pixels x 128 channels (2 x 4 tiles of v_mfma_f32_32x32x16, 128 accumulators);
-//  * K order: channel blocks of 32 (64 B), 9 taps each. The (TH+2) x (TW+2) input halo of one
-//    channel block moves into LDS ONCE (buffer_load ... lds: out-of-image and pad slots are
-//    buffer-OOB, so they read as zero with no per-lane branches) and the 9 taps read shifted
-//    windows of it at compile-time immediate ds_read offsets: 1.2x input traffic instead of 9x;
-//  * two halo buffers (the next channel block — or the next tile's first — streams in during
-//    taps 0..5 of the current one), a 3-slot weight ring (8 KiB per k-step from a k-step-major,
-//    pre-swizzled copy of the weights: each wave's 1 KiB piece is contiguous; loaded into
-//    registers five k-steps ahead (4 register sets) and written with ds_write_b128 two steps
-//    before use — deep enough for the few-tile layers that stream weights from HBM), one raw
-//    s_barrier per k-step with an exact counted vmcnt;
-//  * fragment reads run one 16-deep sub-step ahead of the MFMAs (6 ds_read_b128 per half
-//    k-step, two register sets) and the k-step's LDS-DMA pieces are issued between MFMA pairs;
-//  * the epilogue stores straight from the accumulators (bias from LDS, activation, fp16/bf16
-//    pack, v_permlane32_swap pairs into 16-byte stores), so the next tile's prefetched halo and
-//    weights are already in flight while it runs: no per-tile prologue, no LDS staging.
-// LDS: halo 2 x 48 KiB (pixel pitch 80 B = 64 B of channels + 16 B pad: conflict-free
-// ds_read_b128 for 32-pixel rows), weight ring 3 x 8 KiB (XOR-swizzled 64 B rows), bias.
-#include "conv_common.h"
-
-#include <type_traits>
+// conv3x3.hip — weight repack, tile geometry and the dispatch of the persistent halo-tile 3x3
+// kernel (conv3x3_kernel.h; instances in conv3x3_n2/n4/n8.hip).
+#include "conv3x3_kernel.h"
 
 namespace tv {
 namespace c3 {
-
-constexpr int NT = 512, NW = 8, BN = 128, P = 512;
-constexpr int WP = P / NW;                    // pixels per wave = 64 (two 32-pixel fragments)
-constexpr int CBK = 32;                       // channels per k-step
-// NCB: channel blocks per tile = C / 32 (4 for the 128-channel DLA levels, 8 for 256-channel inputs:
-// the YOLACT protonet's 3x3 convs, DLA-34's 256-channel level)
-template <int RES, int NCB = 4>
-constexpr int spt() { return (9 + RES) * NCB; }
-constexpr int PITCH = 80;                     // halo pixel pitch (bytes)
-constexpr int HPIX = 612;                     // (16+2)x(32+2) = (32+2)x(16+2) halo pixels
-constexpr int HPIECES = 48;                   // ceil(612 * 5 / 64) LDS-DMA pieces of 1 KiB
-constexpr int HBUF = HPIECES * 1024;          // one halo buffer
-constexpr int HPW = HPIECES / NW;             // halo pieces per wave per channel block = 6
-constexpr int HTAPS = HPW;                    // one halo piece per k-step, taps 0..5
-constexpr int WSLOT = BN * 64;                // weights of one k-step: 128 rows x 64 B
-constexpr int RING = 3;                       // weight ring slots (register-staged: k-step q is
-                                              // loaded at step q-3, written to LDS at step q-2)
-constexpr int OFF_W = 2 * HBUF;
-constexpr int OFF_B = OFF_W + RING * WSLOT;
-constexpr int OFF_R = OFF_B + kConv3MaxN * 4;  // RES: one channel block of the residual input
-constexpr int RBUF = 512 * 64;                  // 512 pixels x 32 channels (XOR-swizzled 16 B chunks)
-constexpr int RPW = RBUF / 1024 / NW;           // residual pieces per wave per channel block = 4
-template <int RES>
-constexpr int lds_bytes() { return OFF_R + (RES ? RBUF : 0); }
-static_assert(lds_bytes<1>() <= 160 * 1024, "LDS budget");
-static_assert(WSLOT / 1024 == NW, "one weight piece per wave per k-step");
-static_assert(HPIECES * 64 >= HPIX * 5, "halo pieces");
-
-typedef __attribute__((address_space(3))) char lds_char;
-typedef const __attribute__((address_space(1))) void gvoid;
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-
-__device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-__device__ u32x2 raw_buffer_load_v2(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
-__device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
-__device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
-                                    int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
-
-__device__ __forceinline__ void dma16(const void* src, lds_char* dst) {
-  __builtin_amdgcn_global_load_lds((gvoid*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-}
-template <int OFF>
-__device__ __forceinline__ u32x4 ds_read16(unsigned addr) {
-  u32x4 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
-  return v;
-}
-__device__ __forceinline__ uint4 to_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// s_waitcnt takes an immediate: dispatch the (wave-uniform, exact) count
-__device__ __forceinline__ void wait_vm_n(int n) {
-  switch (n) {
-    case 0: wait_vm<0>(); break;
-    case 1: wait_vm<1>(); break;
-    case 2: wait_vm<2>(); break;
-    case 3: wait_vm<3>(); break;
-    case 4: wait_vm<4>(); break;
-    default: wait_vm<5>(); break;
-  }
-}
-
-template <int V>
-using IC = std::integral_constant<int, V>;
-
-template <int NI>
-struct Half {  // fragments of one 16-deep sub-step
-  u32x4 x[2];    // pixel fragments f
-  u32x4 w[NI];   // channel fragments i
-};
-
-// 16-byte store of 8 channels from two MFMA register groups (k, k+1) of one 32x32 tile:
-// lanes 0-31 hold channels 8k+0..3 (group k) / 8k+8..11 (group k+1) of pixel l, lanes 32-63
-// the +4 halves; one v_permlane32_swap per dword pair gives every lane 8 consecutive channels
-// (lanes 0-31: group k, lanes 32-63: group k+1 of pixel l-32), stored at +8*lh channels.
-template <typename T>
-__device__ __forceinline__ unsigned pack2(float a, float b) {
-  typedef T t2 __attribute__((ext_vector_type(2)));
-  return __builtin_bit_cast(unsigned, t2{(T)a, (T)b});
-}
-template <typename T>
-__device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh) {
-  const unsigned a0 = pack2<T>(v[0][0], v[0][1]), a1 = pack2<T>(v[0][2], v[0][3]);
-  const unsigned b0 = pack2<T>(v[1][0], v[1][1]), b1 = pack2<T>(v[1][2], v[1][3]);
-  const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-  const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-  gstore16(dst + 8 * lh, make_uint4(r0[0], r1[0], r0[1], r1[1]));
-}
-
-// NI: 32-channel fragments per wave — 4 (a 128-channel tile) or 2 (a 64-channel half tile, twice
-// the work units for layers whose 128-channel tiles leave the last round of CUs mostly idle)
-template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI, int NCB>
-__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
-    const ConvParams* __restrict__ pp, void* out_ptr) {
-  static_assert(NI == 4 || (NI == 2 && EPI == 0), "half tiles: plain epilogue only");
-  static_assert(!RES || NCB == 4, "residual k-steps: 128-channel inputs only");
-  constexpr int SPTK = spt<RES, NCB>();  // k-steps per tile
-  constexpr int BNK = 32 * NI;      // output channels per tile
-  constexpr int WSL = BNK * 64;     // weight bytes per k-step (an LDS ring slot holds up to WSLOT)
-  constexpr int WPL = WSL / 512;    // weight bytes per lane per k-step (16 or 8)
-  using WReg = typename std::conditional<NI == 4, u32x4, u32x2>::type;
-  constexpr int TH = P / TW;
-  constexpr int RS = TW + 2;                               // halo row stride (pixels)
-  constexpr int FOFF = (TW == 32 ? 1 : 2) * RS * PITCH;    // next 32-pixel fragment
-  static_assert((TH + 2) * RS == HPIX, "halo shape");
-  const ConvParams& p = *pp;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  lds_char* lds = (lds_char*)smem;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, lh = lane >> 5;
-
-  const ConvSegment& sg = p.seg[0];
-  const int H = sg.H, W = sg.W, ldc = sg.ldc;
-  const int tiles_x = (W + TW - 1) / TW;
-  const int tiles_f = ((H + TH - 1) / TH) * tiles_x;
-  const int ntiles = p.ntiles * (4 / NI);  // channel tiles of BNK (p.ntiles counts 128-channel tiles)
-  const int ntot = p.mtiles * ntiles;
-  [[maybe_unused]] const unsigned long long out_frame_bytes = (unsigned long long)H * W * p.out_ldc * sizeof(OutT);  // < 2^31 (host)
-
-  // ---- this block's tiles: XCD-aware contiguous ranges
-  const int G = gridDim.x, bid = blockIdx.x;
-  int first, stride, end;
-  if ((G & 7) == 0) {
-    first = (int)((long long)ntot * (bid & 7) / 8) + (bid >> 3);
-    end = (int)((long long)ntot * ((bid & 7) + 1) / 8);
-    stride = G >> 3;
-  } else {
-    first = bid;
-    end = ntot;
-    stride = G;
-  }
-  const int ntl = first < end ? (end - first + stride - 1) / stride : 0;
-  if (ntl == 0) return;
-  const int S_tot = ntl * SPTK;
-
-  // bias of every output channel into LDS (read in the epilogues)
-  float* lbias = reinterpret_cast<float*>(smem + OFF_B);
-  for (int c = tid; c < ntiles * BN; c += NT) lbias[c] = c < p.N ? p.bias[c] : 0.0f;
-
-  // ---- sources
-  i32x4 rsrc;
-  {
-    const unsigned long long a = (unsigned long long)sg.src;
-    rsrc.x = (int)(unsigned)a;
-    rsrc.y = (int)(unsigned)(a >> 32);
-    rsrc.z = (int)(unsigned)((unsigned long long)p.M * ldc * sizeof(T));  // bytes (host checks < 2^31)
-    rsrc.w = 0x00020000;
-  }
-  // k-step-major weights: [ntile][k-step][BNK rows][64 B], chunks pre-swizzled; one WSL/8 piece
-  // per wave per k-step at (ntile * SPT + q) * WSL + wave * WSL / 8
-  // (read through a buffer resource: one lane-offset VGPR, the k-step offset in an SGPR)
-  i32x4 wrsrc;
-  {
-    const unsigned long long a = (unsigned long long)p.weight;
-    wrsrc.x = (int)(unsigned)a;
-    wrsrc.y = (int)(unsigned)(a >> 32);
-    wrsrc.z = ntiles * SPTK * WSL;
-    wrsrc.w = 0x00020000;
-  }
-  const int wvoff = wave * (WSL / 8) + lane * WPL;
-
-  // ---- tile decode
-  auto tile_of = [&](int idx, int& fr, int& y0, int& x0, int& nt) __attribute__((always_inline)) {
-    const int t = first + idx * stride;
-    nt = t % ntiles;
-    const int mt = t / ntiles;
-    fr = mt / tiles_f;
-    const int r = mt - fr * tiles_f;
-    const int ty = r / tiles_x;
-    y0 = ty * TH;
-    x0 = (r - ty * tiles_x) * TW;
-  };
-
-  // ---- halo DMA: chunk g = piece*64 + lane -> halo pixel g/5, slot g%5 (slot 4 = pad).
-  // Tile-independent geometry packed once per lane and piece: hy<<16 | hx<<8 | slot, or ~0.
-  unsigned hgeo[HPW], hoff[HPW];
-#pragma unroll
-  for (int i = 0; i < HPW; ++i) {
-    const int g = (wave * HPW + i) * 64 + lane;
-    const int h = g / 5, s5 = g - (g / 5) * 5;
-    const int hy = h / RS, hx = h - (h / RS) * RS;
-    hgeo[i] = (s5 < 4 && h < HPIX) ? (unsigned)((hy << 16) | (hx << 8) | s5) : ~0u;
-  }
-  const unsigned pix_bytes = (unsigned)ldc * (unsigned)sizeof(T);
-  auto halo_offsets = [&](int fr, int y0, int x0) __attribute__((always_inline)) {
-    const int ybase = fr * H;
-#pragma unroll
-    for (int i = 0; i < HPW; ++i) {
-      const unsigned gq = hgeo[i];
-      const int y = y0 - 1 + (int)(gq >> 16);
-      const int x = x0 - 1 + (int)((gq >> 8) & 0xff);
-      const bool ok = gq != ~0u && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
-      hoff[i] = ok ? ((unsigned)(ybase + y) * (unsigned)W + (unsigned)x) * pix_bytes + (gq & 0xff) * 16u
-                   : 0x80000000u;
-    }
-  };
-  // one halo piece (index I of this wave's HPW) of channel block cb into buffer bsel
-  auto halo_piece = [&](auto pc, int cb, int bsel) __attribute__((always_inline)) {
-    constexpr int I = decltype(pc)::value;
-    lds_char* base = lds + bsel * HBUF + (wave * HPW + I) * 1024;
-    raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)base, 16, (int)hoff[I],
-                        cb * CBK * (int)sizeof(T), 0, 0);
-  };
-
-  // ---- RES: the ResidualBlock's 1x1 conv_residual (dla.py:32-37) as a 10th k-step per
-  // channel block. Its input x (second segment, stride rstr) for the tile's 512 output pixels
-  // moves into one 32 KiB LDS buffer per channel block: chunk L = piece*64 + lane holds pixel
-  // q = L/4, source chunk (L % 4) ^ ((q >> 2) & 3) (conflict-free fragment reads). One buffer
-  // resource per frame keeps offsets below 2^31.
-  [[maybe_unused]] unsigned rgeo[RPW];
-  [[maybe_unused]] const ConvSegment& sr = p.seg[RES ? 1 : 0];
-  [[maybe_unused]] const unsigned rpix_bytes = (unsigned)sr.ldc * (unsigned)sizeof(T);
-  if constexpr (RES) {
-#pragma unroll
-    for (int i = 0; i < RPW; ++i) {
-      const int L = (wave * RPW + i) * 64 + lane;
-      const int q = L >> 2;
-      rgeo[i] = (unsigned)((q << 2) | ((L & 3) ^ ((q >> 2) & 3)));
-    }
-  }
-  auto res_piece = [&](int i, int fr, int y0, int x0, int cb) __attribute__((always_inline)) {
-    const unsigned long long fb = (unsigned long long)sr.H * sr.W * rpix_bytes;
-    const unsigned long long a = (unsigned long long)sr.src + (unsigned long long)fr * fb;
-    i32x4 rs;
-    rs.x = (int)(unsigned)a;
-    rs.y = (int)(unsigned)(a >> 32);
-    rs.z = (int)(unsigned)fb;
-    rs.w = 0x00020000;
-    const int q = (int)(rgeo[i] >> 2), c = (int)(rgeo[i] & 3);
-    const int y = y0 + q / TW, x = x0 + q % TW;
-    const bool ok = y < H && x < W;
-    const unsigned off = ok ? ((unsigned)(y * sr.stride) * (unsigned)sr.W + (unsigned)(x * sr.stride)) * rpix_bytes +
-                                  (unsigned)c * 16u
-                            : 0x80000000u;
-    raw_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + OFF_R + (wave * RPW + i) * 1024), 16,
-                        (int)off, cb * CBK * (int)sizeof(T), 0, 0);
-  };
-
-  // ---- weight issue cursor: k-step counter and the global k-step index of the next piece
-  int wc_idx = 0, wc_in = 0, wc_nt = 0;
-  {
-    int a, b_, c_;
-    tile_of(0, a, b_, c_, wc_nt);
-  }
-  // register-staged weights: one 16-byte global load per lane per k-step, written to the
-  // ring slot with ds_write_b128 one step later (instead of an LDS-DMA piece per k-step)
-  WReg wreg[4];  // k-step q's weights are loaded at step q-5 into set q % 4
-  auto w_load = [&](WReg& dst) __attribute__((always_inline)) {
-    if constexpr (NI == 4) dst = raw_buffer_load_v4(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
-    else dst = raw_buffer_load_v2(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
-    if (++wc_in == SPTK) {
-      wc_in = 0;
-      if (++wc_idx < ntl) {
-        int a, b_, c_;
-        tile_of(wc_idx, a, b_, c_, wc_nt);
-      }
-    }
-  };
-
-  // ---- fragment addresses
-  const unsigned lds0 = (unsigned)(uintptr_t)lds;
-  unsigned xa;  // pixel WP*wave + l32 of the tile, tap (0,0), lane-half chunk
-  {
-    const int q = WP * wave + l32;
-    const int r = q / TW, c = q - (q / TW) * TW;
-    xa = lds0 + (unsigned)((r * RS + c) * PITCH + lh * 16);
-  }
-  unsigned wa[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-    wa[j] = lds0 + OFF_W + (unsigned)(l32 * 64 + (((2 * j + lh) ^ ((l32 >> 2) & 3)) << 4));
-
-  // RES: fragment base of pixel q0 = WP*wave + l32 in the residual buffer, per sub-step J
-  // (fragment f = 1 is q0 + 32: +2 KiB, same swizzle)
-  [[maybe_unused]] unsigned rxa[2];
-  if constexpr (RES) {
-    const int q0 = WP * wave + l32;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) rxa[j] = lds0 + OFF_R + (unsigned)(q0 * 64 + (((2 * j + lh) ^ ((q0 >> 2) & 3)) << 4));
-  }
-
-  // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]; TAP 9 = residual k-step
-  auto read_one = [&](auto r, auto j, auto tap, unsigned xb, unsigned wb, Half<NI>& F) __attribute__((always_inline)) {
-    constexpr int R = decltype(r)::value, J = decltype(j)::value, TAP = decltype(tap)::value;
-    if constexpr (TAP == 9) {
-      if constexpr (R < 2) F.x[R] = ds_read16<R * 2048>(rxa[J]);
-      else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
-    } else {
-      constexpr int TOFF = ((TAP / 3) * RS + (TAP % 3)) * PITCH;
-      if constexpr (R < 2) F.x[R] = ds_read16<TOFF + 32 * J + R * FOFF>(xb);
-      else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
-    }
-  };
-
-  f32x16 acc[2][NI];  // [pixel fragment f][channel fragment i]; first written by a tile's first k-step
-
-  // the 2 MFMAs of channel fragment I of one sub-step; FIRST: the tile's first products
-  // (accumulate onto zero instead of clearing the accumulators in the epilogue)
-  auto mfma_pair = [&](auto i, auto first, const Half<NI>& F) __attribute__((always_inline)) {
-    constexpr int I = decltype(i)::value;
-    if constexpr (decltype(first)::value) {
-      acc[0][I] = f32x16{};
-      acc[1][I] = f32x16{};
-    }
-    Mfma<T>::run(to_u4(F.w[I]), to_u4(F.x[0]), acc[0][I]);
-    Mfma<T>::run(to_u4(F.w[I]), to_u4(F.x[1]), acc[1][I]);
-  };
-
-  // ---- epilogue of the tile (fr, y0, x0, nt): straight from the accumulators
-  auto epilogue = [&](int fr, int y0, int x0, int nt) __attribute__((always_inline)) {
-    const int n0 = nt * BNK;
-#pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const int q = WP * wave + 32 * f + l32;
-      const int y = y0 + q / TW, x = x0 + q % TW;
-      const bool ok = y < H && x < W;
-      [[maybe_unused]] OutT* dst = reinterpret_cast<OutT*>(out_ptr) +
-                  ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.out_ldc + p.out_coff + n0;
-      // EPI 0: stores through a per-frame buffer resource, every lane always issuing (invalid
-      // pixels / channels -> OOB offset, dropped): a fixed count of VMEM operations per tile
-      [[maybe_unused]] i32x4 orsrc;
-      [[maybe_unused]] unsigned obase = 0;
-      if constexpr (EPI == 0) {
-        const unsigned long long a = (unsigned long long)out_ptr + (unsigned long long)fr * out_frame_bytes;
-        orsrc.x = (int)(unsigned)a;
-        orsrc.y = (int)(unsigned)(a >> 32);
-        orsrc.z = (int)out_frame_bytes;
-        orsrc.w = 0x00020000;
-        obase = ok ? ((unsigned)(y * W + x) * (unsigned)p.out_ldc + (unsigned)(p.out_coff + n0 + 8 * lh)) * (unsigned)sizeof(OutT)
-                   : 0x80000000u;
-      }
-      [[maybe_unused]] f32x16 hacc = f32x16{};  // EPI 1: the 1x1 heads' partial sums of this pixel
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          float v[2][4];
-#pragma unroll
-          for (int gg = 0; gg < 2; ++gg) {
-            const int G2 = 2 * m + gg;
-            const f32x4 bb = *reinterpret_cast<const f32x4*>(lbias + n0 + 32 * i + 8 * G2 + 4 * lh);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              float t = acc[f][i][4 * G2 + e] + bb[e];
-              if constexpr (ACT == 1) t = fmaxf(t, 0.0f);
-              else if constexpr (ACT == 2) t = fmaxf(t, 0.01f * t);  // == (t >= 0 ? t : 0.01t)
-              v[gg][e] = t;
-            }
-          }
-          if constexpr (EPI == 0) {
-            const int ch = n0 + 32 * i + 16 * m;
-            const unsigned a0 = pack2<OutT>(v[0][0], v[0][1]), a1 = pack2<OutT>(v[0][2], v[0][3]);
-            const unsigned b0 = pack2<OutT>(v[1][0], v[1][1]), b1 = pack2<OutT>(v[1][2], v[1][3]);
-            const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-            const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-            raw_buffer_store_v4(u32x4{r0[0], r1[0], r0[1], r1[1]}, orsrc,
-                                ch < p.N ? (int)(obase + (unsigned)((32 * i + 16 * m) * sizeof(OutT))) : (int)0x80000000u, 0, 0);
-          } else {
-            // the 8 hidden channels 32i+16m+8lh.. of this pixel, rounded to T exactly as the
-            // unfused path stores them, are the MFMA B operand of k-step 2i+m of the 1x1
-            const unsigned a0 = pack2<T>(v[0][0], v[0][1]), a1 = pack2<T>(v[0][2], v[0][3]);
-            const unsigned b0 = pack2<T>(v[1][0], v[1][1]), b1 = pack2<T>(v[1][2], v[1][3]);
-            const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-            const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-            const uint4 hv = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-            const uint4 hwf = gload16(reinterpret_cast<const char*>(p.head_w) +
-                                      ((size_t)(nt * 8 + 2 * i + m) * 64 + lane) * 16);
-            Mfma<T>::run(hwf, hv, hacc);
-          }
-          __builtin_amdgcn_sched_barrier(0);  // bound the live set: one 8-channel group at a time
-        }
-      }
-      if constexpr (EPI == 1) {
-        // rows r = 8G + 4lh + e of the 1x1 result: output column head_row0[nt] + r of pixel (y, x)
-        const int nr = p.head_nrows[nt];
-        float* hd = reinterpret_cast<float*>(out_ptr) + ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.head_ldc +
-                    p.head_row0[nt];
-        const float* hb = p.head_b + nt * 32;
-#pragma unroll
-        for (int G = 0; G < 4; ++G)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 8 * G + 4 * lh + e;
-            if (ok && r < nr) unsafeAtomicAdd(hd + r, hacc[4 * G + e] + hb[r]);
-          }
-      }
-    }
-  };
-
-  // ---- prologue: halo of (tile 0, block 0), weights of k-steps 0..2
-  int cur_fr, cur_y0, cur_x0, cur_nt;
-  tile_of(0, cur_fr, cur_y0, cur_x0, cur_nt);
-  halo_offsets(cur_fr, cur_y0, cur_x0);
-  halo_piece(IC<0>{}, 0, 0);
-  halo_piece(IC<1>{}, 0, 0);
-  halo_piece(IC<2>{}, 0, 0);
-  halo_piece(IC<3>{}, 0, 0);
-  halo_piece(IC<4>{}, 0, 0);
-  halo_piece(IC<5>{}, 0, 0);
-  __builtin_amdgcn_sched_barrier(0);  // the counted wait below needs the halo issued first
-  // weights: k-steps 0, 1 into ring slots 0, 1; k-steps 2, 3, 4 in flight in sets 2, 3, 0
-  // (S_tot >= SPTK > 5). Every VMEM operation of the main loop is issued unconditionally —
-  // past the end of the list the weight loads re-read the last tile's k-steps and the halo
-  // pieces reload the current tile into the idle buffer — so that the compiler's own vmcnt
-  // for each weight ds_write is exact: a conditional load makes it fall back to vmcnt(0),
-  // which drains the halo pieces and weight loads issued since (measured: ~20% of the layer).
-  w_load(wreg[0]);
-  w_load(wreg[1]);
-  *reinterpret_cast<WReg*>(smem + OFF_W + wvoff) = wreg[0];
-  *reinterpret_cast<WReg*>(smem + OFF_W + WSLOT + wvoff) = wreg[1];
-  w_load(wreg[2]);
-  w_load(wreg[3]);
-  w_load(wreg[0]);
-  if constexpr (EPI == 0) {
-    // as many (dropped: zero-size resource) stores as a tile epilogue issues, so that both paths
-    // into the tile loop carry the same VMEM sequence and the compiler's vmcnt for the first
-    // weight ds_writes of a tile leaves the previous tile's stores in flight
-    __builtin_amdgcn_sched_barrier(0);
-    i32x4 nul;
-    nul.x = (int)(unsigned)(unsigned long long)out_ptr;
-    nul.y = (int)(unsigned)((unsigned long long)out_ptr >> 32);
-    nul.z = 0;
-    nul.w = 0x00020000;
-#pragma unroll
-    for (int k = 0; k < 4 * NI; ++k) raw_buffer_store_v4(u32x4{0u, 0u, 0u, 0u}, nul, k * 16, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  // the halo (issued first) landed; the weights of k-steps 2..4 (and the dropped stores) may stay in flight
-  wait_vm<EPI == 0 ? 3 + 4 * NI : 3>();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-
-  Half<NI> H0, H1;  // sub-step 0 / 1 fragments
-  read_one(IC<0>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<1>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<2>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<3>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  if constexpr (NI == 4) {
-    read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-    read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  }
-
-  int s = 0;   // global k-step
-  int tl = 0;  // tile index within this block's list
-  int cb = 0;  // channel block within the tile (compile-time inside cblock)
-  // the channel block after the current one: same tile cb+1, or the next tile's block 0
-  bool nxt_exists = true, nxt_newtile = false;
-
-  // One k-step with compile-time tap. On entry H0 holds its sub-step-0 fragments; the first
-  // half (8 MFMAs on H0) overlaps the reads of its sub-step-1 fragments into H1, the second
-  // half (8 MFMAs on H1) the reads of the NEXT k-step's sub-step-0 fragments into H0. The
-  // k-step's LDS-DMA pieces (1 weight, <= 1 halo) are issued between MFMA pairs.
-  // Halo buffer of channel block cb is cb & 1 (NCB is even, so parity is per-tile fixed).
-  auto step = [&](auto tap, auto first, auto par) __attribute__((always_inline)) {
-    constexpr int TAP = decltype(tap)::value;
-    // Weights of k-step s+1 were written to LDS at step s-1 (lgkmcnt + barrier below); halo and
-    // residual data arrive by LDS-DMA and are waited for with an exact vmcnt: the count of
-    // vector-memory operations issued after the last piece the next k-step reads. A weight load
-    // is issued at every step q >= 0; within a step the order is halo piece (taps 0..5, next
-    // channel block), residual piece (RES, taps 1..4, this channel block), weight load.
-    //  * tap 8 without RES / residual step (tap 9): the next k-step reads the NEXT channel
-    //    block's halo (last piece at tap 5): younger = the weight loads of taps 5, 6, 7 (and 8);
-    //  * tap 8 with RES: the residual step reads this block's residual input (last piece at
-    //    tap 4): younger = weight loads of taps 4, 5, 6, 7 + the tap-5 halo piece.
-    static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
-    auto wl = [&](int q) { return q >= 0 ? 1 : 0; };
-    if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
-    if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
-    if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-
-    constexpr int NTAP = TAP == 8 ? (RES ? 9 : 0) : TAP == 9 ? 0 : TAP + 1;
-    const bool do_r = s + 1 < S_tot;
-    const int hbuf = (cb + 1) & 1;
-    const unsigned xc = xa + (cb & 1) * HBUF;                                  // this k-step's halo
-    const unsigned xn = xa + (NTAP == 0 ? hbuf : (cb & 1)) * HBUF;             // next k-step's halo
-    const unsigned wc1 = wa[1] + (unsigned)((s % RING) * WSLOT);
-    const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
-    // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
-    constexpr bool FIRST = TAP == 0 && decltype(first)::value;
-    constexpr int PAR = decltype(par)::value;  // s % 4 (36 or 40 k-steps per tile: static)
-    mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
-    read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
-    read_one(IC<2>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    read_one(IC<3>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    // k-step s+2 (loaded at step s-3) into its ring slot: it last held k-step s-1, read
-    // completely before this step's barrier (past the end: an unread slot)
-    *reinterpret_cast<WReg*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wvoff) = wreg[(PAR + 2) & 3];
-    if constexpr (TAP == 0) {
-      if (nxt_exists && nxt_newtile) {
-        int fr, y0, x0, nt;
-        tile_of(tl + 1, fr, y0, x0, nt);
-        halo_offsets(fr, y0, x0);
-      }
-    }
-    if constexpr (NI == 4) {
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_pair(IC<2>{}, IC<FIRST>{}, H0);
-      read_one(IC<4>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-      read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
-    }
-    if constexpr (TAP < HTAPS)
-      halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);  // (no next block: the idle buffer)
-    if constexpr (RES && TAP >= 1 && TAP <= RPW) res_piece(TAP - 1, cur_fr, cur_y0, cur_x0, cb);
-    if constexpr (NI == 4) {
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_pair(IC<3>{}, IC<FIRST>{}, H0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<0>{}, IC<false>{}, H1);
-    // k-step s+5 into the set whose k-step s+1 went to LDS at step s-1. Issued here, after the
-    // halo/residual pieces and away from the barrier where all 8 waves issue at once (-4%)
-    w_load(wreg[(PAR + 1) & 3]);
-    if (do_r) {
-      read_one(IC<0>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-      read_one(IC<1>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<1>{}, IC<false>{}, H1);
-    if (do_r) {
-      read_one(IC<2>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-      read_one(IC<3>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-    }
-    if constexpr (NI == 4) {
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_pair(IC<2>{}, IC<false>{}, H1);
-      if (do_r) {
-        read_one(IC<4>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-        read_one(IC<5>{}, IC<0>{}, IC<NTAP>{}, xn, wn0, H0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_pair(IC<3>{}, IC<false>{}, H1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    ++s;
-  };
-
-  auto cblock = [&](auto cbc) __attribute__((always_inline)) {
-    constexpr int CB = decltype(cbc)::value;
-    cb = CB;
-    nxt_newtile = CB + 1 == NCB;
-    nxt_exists = !nxt_newtile || tl + 1 < ntl;
-    constexpr int P0 = CB * (9 + RES);  // k-step index of the block's tap 0 within the tile
-    step(IC<0>{}, IC<CB == 0>{}, IC<(P0 + 0) & 3>{});
-    step(IC<1>{}, IC<false>{}, IC<(P0 + 1) & 3>{});
-    step(IC<2>{}, IC<false>{}, IC<(P0 + 2) & 3>{});
-    step(IC<3>{}, IC<false>{}, IC<(P0 + 3) & 3>{});
-    step(IC<4>{}, IC<false>{}, IC<(P0 + 4) & 3>{});
-    step(IC<5>{}, IC<false>{}, IC<(P0 + 5) & 3>{});
-    step(IC<6>{}, IC<false>{}, IC<(P0 + 6) & 3>{});
-    step(IC<7>{}, IC<false>{}, IC<(P0 + 7) & 3>{});
-    step(IC<8>{}, IC<false>{}, IC<(P0 + 8) & 3>{});
-    if constexpr (RES) step(IC<9>{}, IC<false>{}, IC<(P0 + 9) & 3>{});
-  };
-
-  // NCB channel blocks per tile, fully unrolled (36 / 72 k-steps of straight-line code): the
-  // accumulators keep one register assignment through the whole tile
-  static_assert(NCB % 2 == 0 && SPTK % 4 == 0, "tile body: an even number of channel blocks (halo buffer parity), k-steps per tile a multiple of the 4 weight register sets");
-  auto blocks = [&](auto self, auto i) __attribute__((always_inline)) {
-    constexpr int I = decltype(i)::value;
-    if constexpr (I < NCB) {
-      cblock(IC<I>{});
-      self(self, IC<I + 1>{});
-    }
-  };
-  for (; tl < ntl;) {
-    blocks(blocks, IC<0>{});
-    epilogue(cur_fr, cur_y0, cur_x0, cur_nt);
-    ++tl;
-    if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
-  }
-}
 
 // [Npad][Kpad] (K = tap * 128 + channel) -> [ntile][k-step q][bnk rows][4 x 16 B] (channel tiles
 // of bnk = 128 or 64 rows), q = cb*9 + tap (res: q = cb*10 + j, j = 9 the residual segment's
@@ -643,24 +21,6 @@ __global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntil
   }
 }
 
-template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4, int NCB = 4>
-static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
-  auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>;
-  constexpr int lds = lds_bytes<RES>();
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) {
-      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-      return 3;
-    }
-    attr = true;
-  }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, out);
-  TV_HIP(hipGetLastError());
-  return 0;
-}
-
 }  // namespace c3
 
 int conv3x3_tiles(int B, int H, int W, int tw) {
@@ -673,7 +33,7 @@ size_t conv3x3_weight_bytes(int ntiles, int res, int ncb) {
 }
 
 int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, void* out, hipStream_t s) {
-  if ((Kpad * esz) % 16 || Kpad < (9 + res) * 32 * ncb || (ni != 4 && ni != 2) || (ncb != 4 && ncb != 8) ||
+  if ((Kpad * esz) % 16 || Kpad < (9 + res) * 32 * ncb || (ni != 4 && ni != 2) || (ncb != 2 && ncb != 4 && ncb != 8) ||
       (res && ncb != 4)) {
     set_error("conv3x3_repack: bad Kpad / ni / channel blocks");
     return 1;
@@ -692,75 +52,13 @@ int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dty
     return 1;
   }
   const int ncb = p.seg[0].C / CBK;
-  if ((ncb != 4 && ncb != 8) || (ncb == 8 && res)) {
-    set_error("conv3x3: inputs of 128 or 256 channels (residual k-steps: 128)");
+  if ((ncb != 2 && ncb != 4 && ncb != 8) || (ncb != 4 && res)) {
+    set_error("conv3x3: inputs of 64, 128 or 256 channels (residual k-steps: 128)");
     return 1;
   }
-  using L = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
-  if (ncb == 8) {  // 256-channel inputs (protonet, DLA-34 level 4)
-    if (epi == 1) {
-      if (p.act != 2 || p.ntiles > 8) {
-        set_error("conv3x3: fused 1x1 needs LeakyReLU and <= 8 channel tiles");
-        return 1;
-      }
-      if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 2, 1, 0, 4, 8>(p, dp, out, grid, s) : launch_t<_Float16, 16, 2, 1, 0, 4, 8>(p, dp, out, grid, s);
-      if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 2, 1, 0, 4, 8>(p, dp, out, grid, s) : launch_t<__bf16, 16, 2, 1, 0, 4, 8>(p, dp, out, grid, s);
-      set_error("conv3x3: fp16/bf16 only");
-      return 1;
-    }
-    static const L f8[2][2][3] = {
-        {{launch_t<_Float16, 16, 0, 0, 0, 2, 8>, launch_t<_Float16, 16, 1, 0, 0, 2, 8>, launch_t<_Float16, 16, 2, 0, 0, 2, 8>},
-         {launch_t<_Float16, 32, 0, 0, 0, 2, 8>, launch_t<_Float16, 32, 1, 0, 0, 2, 8>, launch_t<_Float16, 32, 2, 0, 0, 2, 8>}},
-        {{launch_t<_Float16, 16, 0, 0, 0, 4, 8>, launch_t<_Float16, 16, 1, 0, 0, 4, 8>, launch_t<_Float16, 16, 2, 0, 0, 4, 8>},
-         {launch_t<_Float16, 32, 0, 0, 0, 4, 8>, launch_t<_Float16, 32, 1, 0, 0, 4, 8>, launch_t<_Float16, 32, 2, 0, 0, 4, 8>}}};
-    static const L b8[2][2][3] = {
-        {{launch_t<__bf16, 16, 0, 0, 0, 2, 8>, launch_t<__bf16, 16, 1, 0, 0, 2, 8>, launch_t<__bf16, 16, 2, 0, 0, 2, 8>},
-         {launch_t<__bf16, 32, 0, 0, 0, 2, 8>, launch_t<__bf16, 32, 1, 0, 0, 2, 8>, launch_t<__bf16, 32, 2, 0, 0, 2, 8>}},
-        {{launch_t<__bf16, 16, 0, 0, 0, 4, 8>, launch_t<__bf16, 16, 1, 0, 0, 4, 8>, launch_t<__bf16, 16, 2, 0, 0, 4, 8>},
-         {launch_t<__bf16, 32, 0, 0, 0, 4, 8>, launch_t<__bf16, 32, 1, 0, 0, 4, 8>, launch_t<__bf16, 32, 2, 0, 0, 4, 8>}}};
-    if (dtype == F16) return f8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-    if (dtype == BF16) return b8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-    set_error("conv3x3: fp16/bf16 only");
-    return 1;
-  }
-  if (res) {  // ResidualBlock conv2 + conv_residual: ReLU, plain stores
-    if (p.act != 1 || epi != 0 || p.nseg != 2 || p.ntiles != 1) {
-      set_error("conv3x3: residual k-steps need ReLU, one channel tile and two segments");
-      return 1;
-    }
-    static const L r16[2][2] = {{launch_t<_Float16, 16, 1, 0, 1, 2>, launch_t<_Float16, 16, 1, 0, 1, 4>},
-                                {launch_t<_Float16, 32, 1, 0, 1, 2>, launch_t<_Float16, 32, 1, 0, 1, 4>}};
-    static const L rb16[2][2] = {{launch_t<__bf16, 16, 1, 0, 1, 2>, launch_t<__bf16, 16, 1, 0, 1, 4>},
-                                 {launch_t<__bf16, 32, 1, 0, 1, 2>, launch_t<__bf16, 32, 1, 0, 1, 4>}};
-    if (dtype == F16) return r16[tw == 32][ni == 4](p, dp, out, grid, s);
-    if (dtype == BF16) return rb16[tw == 32][ni == 4](p, dp, out, grid, s);
-    set_error("conv3x3: fp16/bf16 only");
-    return 1;
-  }
-  if (epi == 1) {  // fused 1x1 heads: the stacked heads' LeakyReLU only
-    if (p.act != 2 || p.ntiles > 8) {
-      set_error("conv3x3: fused heads need LeakyReLU and <= 8 channel tiles");
-      return 1;
-    }
-    if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 2, 1>(p, dp, out, grid, s) : launch_t<_Float16, 16, 2, 1>(p, dp, out, grid, s);
-    if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 2, 1>(p, dp, out, grid, s) : launch_t<__bf16, 16, 2, 1>(p, dp, out, grid, s);
-    set_error("conv3x3: fp16/bf16 only");
-    return 1;
-  }
-  static const L f16[2][2][3] = {
-      {{launch_t<_Float16, 16, 0, 0, 0, 2>, launch_t<_Float16, 16, 1, 0, 0, 2>, launch_t<_Float16, 16, 2, 0, 0, 2>},
-       {launch_t<_Float16, 32, 0, 0, 0, 2>, launch_t<_Float16, 32, 1, 0, 0, 2>, launch_t<_Float16, 32, 2, 0, 0, 2>}},
-      {{launch_t<_Float16, 16, 0>, launch_t<_Float16, 16, 1>, launch_t<_Float16, 16, 2>},
-       {launch_t<_Float16, 32, 0>, launch_t<_Float16, 32, 1>, launch_t<_Float16, 32, 2>}}};
-  static const L b16[2][2][3] = {
-      {{launch_t<__bf16, 16, 0, 0, 0, 2>, launch_t<__bf16, 16, 1, 0, 0, 2>, launch_t<__bf16, 16, 2, 0, 0, 2>},
-       {launch_t<__bf16, 32, 0, 0, 0, 2>, launch_t<__bf16, 32, 1, 0, 0, 2>, launch_t<__bf16, 32, 2, 0, 0, 2>}},
-      {{launch_t<__bf16, 16, 0>, launch_t<__bf16, 16, 1>, launch_t<__bf16, 16, 2>},
-       {launch_t<__bf16, 32, 0>, launch_t<__bf16, 32, 1>, launch_t<__bf16, 32, 2>}}};
-  if (dtype == F16) return f16[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-  if (dtype == BF16) return b16[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-  set_error("conv3x3: fp16/bf16 only");
-  return 1;
+  if (ncb == 2) return launch_ncb2(p, dp, out, dtype, tw, grid, s, epi, ni);
+  if (ncb == 8) return launch_ncb8(p, dp, out, dtype, tw, grid, s, epi, ni);
+  return launch_ncb4(p, dp, out, dtype, tw, grid, s, epi, res, ni);
 }
 
 }  // namespace tv

@@ -1,0 +1,38 @@
+// conv3x3 instances for 256-channel inputs (NCB = 8): the YOLACT protonet, DLA-34 level 4
+#include "conv3x3_kernel.h"
+
+namespace tv {
+namespace c3 {
+
+int launch_ncb8(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s, int epi,
+                int ni) {
+  // 256-channel inputs (protonet, DLA-34 level 4)
+    if (epi == 1) {
+      if (p.act != 2 || p.ntiles > 16) {
+        set_error("conv3x3: fused 1x1 needs LeakyReLU and <= 16 channel tiles");
+        return 1;
+      }
+      if (dtype == F16) return tw == 32 ? launch_t<_Float16, 32, 2, 1, 0, 4, 8>(p, dp, out, grid, s) : launch_t<_Float16, 16, 2, 1, 0, 4, 8>(p, dp, out, grid, s);
+      if (dtype == BF16) return tw == 32 ? launch_t<__bf16, 32, 2, 1, 0, 4, 8>(p, dp, out, grid, s) : launch_t<__bf16, 16, 2, 1, 0, 4, 8>(p, dp, out, grid, s);
+      set_error("conv3x3: fp16/bf16 only");
+      return 1;
+    }
+    static const Launch f8[2][2][3] = {
+        {{launch_t<_Float16, 16, 0, 0, 0, 2, 8>, launch_t<_Float16, 16, 1, 0, 0, 2, 8>, launch_t<_Float16, 16, 2, 0, 0, 2, 8>},
+         {launch_t<_Float16, 32, 0, 0, 0, 2, 8>, launch_t<_Float16, 32, 1, 0, 0, 2, 8>, launch_t<_Float16, 32, 2, 0, 0, 2, 8>}},
+        {{launch_t<_Float16, 16, 0, 0, 0, 4, 8>, launch_t<_Float16, 16, 1, 0, 0, 4, 8>, launch_t<_Float16, 16, 2, 0, 0, 4, 8>},
+         {launch_t<_Float16, 32, 0, 0, 0, 4, 8>, launch_t<_Float16, 32, 1, 0, 0, 4, 8>, launch_t<_Float16, 32, 2, 0, 0, 4, 8>}}};
+    static const Launch b8[2][2][3] = {
+        {{launch_t<__bf16, 16, 0, 0, 0, 2, 8>, launch_t<__bf16, 16, 1, 0, 0, 2, 8>, launch_t<__bf16, 16, 2, 0, 0, 2, 8>},
+         {launch_t<__bf16, 32, 0, 0, 0, 2, 8>, launch_t<__bf16, 32, 1, 0, 0, 2, 8>, launch_t<__bf16, 32, 2, 0, 0, 2, 8>}},
+        {{launch_t<__bf16, 16, 0, 0, 0, 4, 8>, launch_t<__bf16, 16, 1, 0, 0, 4, 8>, launch_t<__bf16, 16, 2, 0, 0, 4, 8>},
+         {launch_t<__bf16, 32, 0, 0, 0, 4, 8>, launch_t<__bf16, 32, 1, 0, 0, 4, 8>, launch_t<__bf16, 32, 2, 0, 0, 4, 8>}}};
+    if (dtype == F16) return f8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
+    if (dtype == BF16) return b8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
+    set_error("conv3x3: fp16/bf16 only");
+    return 1;
+  
+}
+
+}  // namespace c3
+}  // namespace tv

@@ -226,7 +226,7 @@ int Engine::pack_op(size_t oi) {
     const int K = plan.tensors[op.segs[0].src].C;  // hidden channels
     const int nts = K / 128;
     const int hid = K / (int)op.stack_w.size();    // hidden channels per head
-    bool ok = K % 128 == 0 && nts <= 8 && hid % 128 == 0;
+    bool ok = K % 128 == 0 && nts <= 16 && hid % 128 == 0;
     for (size_t h = 0; h < op.stack_n.size(); ++h) ok = ok && op.stack_n[h] <= 32;
     if (ok) {
       std::vector<uint8_t> frag((size_t)nts * 8 * 64 * 16, 0);
@@ -527,7 +527,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
       const size_t src_bytes = (size_t)B * cs.H * cs.W * cs.ldc * esz;
       if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand &&
-          (cs.C == 128 || (cs.C == 256 && !res2)) &&
+          (cs.C == 128 || ((cs.C == 256 || cs.C == 64) && !res2)) &&
           cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && src_bytes < (1ull << 31) &&
           p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix &&
           (size_t)cs.H * cs.W * p.out_ldc * esz < (1ull << 31)) {
@@ -540,9 +540,10 @@ int Engine::make_workspace(int B, Workspace* ws) {
         const long t4 = (long)mt * p.ntiles;
         const long r4 = (t4 + cu_count - 1) / cu_count, r2 = (2 * t4 + cu_count - 1) / cu_count;
         int ni = c3_ni_force ? c3_ni_force : (c3_half_cost > 0 && c3_half_cost * r2 < 100 * r4) ? 2 : 4;
-        if (op.act == 2 && !res && op.out >= 0 && i + 1 < plan.ops.size() && !plan.ops[i + 1].diag_in_off.empty())
+        if (p.N <= 64 && !res) ni = 2;  // one 64-channel half tile holds every output channel
+        if (op.act >= 1 && !res && op.out >= 0 && i + 1 < plan.ops.size() && !plan.ops[i + 1].diag_in_off.empty())
           ni = 4;  // the stacked heads (fused 1x1 epilogue) keep 128-channel tiles
-        const long total = t4 * (4 / ni);
+        const long total = (ni == 2 && p.N <= 64) ? t4 : t4 * (4 / ni);
         int grid = (int)std::min<long>(total, cu_count);
         // XCD-aware contiguous ranges need a multiple of 8 workgroups; rounding down is only
         // worth it when every workgroup still gets several units (measured at B=1: 20 units on
@@ -599,13 +600,14 @@ int Engine::make_workspace(int B, Workspace* ws) {
     const OpSpec& h2 = plan.ops[i + 1];
     const Packed& pk2 = packed[i + 1];
     if (!ws->c3_tw[i] || ws->c3_ni[i] != 4 || h2.diag_in_off.empty() || !pk2.head_ok || h2.out >= 0 || h2.segs[0].src != plan.ops[i].out ||
-        plan.ops[i].act != 2 || ws->params[i].ntiles != plan.ops[i].N / 128)
+        (plan.ops[i].act != 2 && !(plan.ops[i].act == 1 && plan.tensors[plan.ops[i].segs[0].src].C == 64)) ||
+        ws->params[i].ntiles != plan.ops[i].N / 128)
       continue;
     ConvParams& p = ws->params[i];
     p.head_w = pk2.head_w;
     p.head_b = pk2.head_b;
     p.head_ldc = plan.out_cpad;
-    for (int t = 0; t < 8; ++t) {
+    for (int t = 0; t < 16; ++t) {
       p.head_row0[t] = pk2.head_row0[t];
       p.head_nrows[t] = pk2.head_nrows[t];
     }

@@ -23,7 +23,7 @@ struct Packed {
   int head_ok = 0;
   void* head_w = nullptr;
   float* head_b = nullptr;
-  int head_row0[8] = {}, head_nrows[8] = {};
+  int head_row0[16] = {}, head_nrows[16] = {};
 };
 
 struct Workspace {

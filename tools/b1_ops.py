@@ -13,8 +13,9 @@ import tauv_vision_amd as tv  # noqa: E402
 
 prec = sys.argv[1] if len(sys.argv) > 1 else "fp16"
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+arch = os.environ.get("OPS_MODEL", "r18")
 dev = torch.device("cuda", 0)
-model, oc, _ = bench.build_model(prec, dev)
+model, oc, _ = bench.build_model(prec, dev, arch)
 eng = model.engine(dev, 480, 640)
 fr = torch.randint(0, 256, (B, 480, 640, 3), dtype=torch.uint8, device=dev)
 out = eng.alloc_out(B)

@@ -111,6 +111,11 @@ int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
                 hipStream_t s);
 
+// Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
+// output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC
+bool conv_small_supported(int cin, int cout, int stride, int cin_ldc, int out_ldc);
+int launch_conv_small(const ConvParams& p, const ConvParams* dp, int dtype, int cu_count, hipStream_t s);
+
 // Fused input staging + 7x7 stem conv (stem.hip), fp16/bf16, C0 <= 128 output channels.
 struct StemParams {
   const void* input;  // u8 NHWC [B,H,W,3] frames (u8 = 1) or normalised fp32 NCHW [B,3,H,W]

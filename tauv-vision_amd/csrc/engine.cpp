@@ -593,6 +593,21 @@ int Engine::make_workspace(int B, Workspace* ws) {
       }
     }
   }
+  // narrow-channel 3x3 convs (16 / 32 input channels) on conv_small.hip
+  ws->small.assign(plan.ops.size(), 0);
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    if (dtype == F32 || op.kind != OP_CONV || op.segs.size() != 1 || op.out < 0 || op.add >= 0 || op.up_s ||
+        ws->c3_tw[i] || ws->s2_grid[i])
+      continue;
+    const SegSpec& sg = op.segs[0];
+    const ConvParams& p = ws->params[i];
+    if (sg.kh == 3 && sg.kw == 3 && sg.pad == 1 && (sg.pad_w < 0 || sg.pad_w == 1) && !sg.row_expand &&
+        conv_small_supported(p.seg[0].C, op.N, sg.stride, p.seg[0].ldc, p.out_ldc) && p.N == op.N) {
+      ws->small[i] = 1;
+      ws->use_pipe[i] = 0;
+    }
+  }
   // stacked 3x3 heads on conv3x3 + block-diagonal 1x1 heads -> one launch (EPI 1)
   ws->head_fused.assign(plan.ops.size(), 0);
   ws->head_skip.assign(plan.ops.size(), 0);
@@ -757,6 +772,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;
+  if (ws->small[i]) return launch_conv_small(p, ws->dparams + i, dtype, cu_count, s);
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
                                            ws->c3_res[i], ws->c3_ni[i])
@@ -894,6 +910,9 @@ const char* Engine::op_kernel(int B, size_t i) {
     if (name.empty()) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
+      else if (ws->small[i])
+        name = std::string("tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
+               std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";

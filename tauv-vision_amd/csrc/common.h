@@ -111,6 +111,24 @@ int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
                 hipStream_t s);
 
+// Fused DCNv2 (dcn.hip), fp16/bf16: bilinear samples x sigmoid(mask) gathered into the MFMA operand
+// tile (no column tensor) x the DeformConv2d weight packed as [Npad][Kpad], K = tap * C + c; bias
+// (BN folded) + activation; NHWC
+struct DcnParams {
+  const void* x;      // input [B, H, W, ldx], C channels used
+  int B, H, W, C, ldx;
+  const void* om;     // offset / mask conv output [B, H, W, om_ldc]: dy, dx per tap (18), mask logits (9)
+  int om_ldc;
+  const void* w;      // [Npad][Kpad]
+  int Kpad;
+  const float* bias;  // [Npad]
+  int act;
+  void* out;          // [B, H, W, out_ldc], N channels
+  int out_ldc, N;
+};
+bool dcn_gemm_supported(int C, int N, int ldx, int om_ldc, int out_ldc);
+int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s);
+
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
 // output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC
 bool conv_small_supported(int cin, int cout, int stride, int cin_ldc, int out_ldc);

@@ -1,0 +1,218 @@
+// Fused DCNv2 (gfx950, fp16 / bf16): DeformConv.forward (centerpoint_dla.py:386-392) =
+// relu(bn(deform_conv2d(x, offset, sigmoid(mask), W) + b)) as ONE kernel — the bilinear samples
+// are gathered straight into the LDS operand tile of the MFMA GEMM instead of a 9 x C column
+// tensor in HBM (dcn_sample + an implicit GEMM over the columns moved 2 x 9C x 2 B per pixel: 1.4 GB
+// per 64-channel layer at 32 frames of 120x160).
+//
+// GEMM view: rows = 64 output channels (A = the DeformConv2d weight, BN folded, K = tap * C + c as
+// the column GEMM packs it), columns = 128 output pixels (B = the sampled values), K in steps of 32
+// (one tap, 32 channels). Workgroup = 4 waves; wave w owns pixels 32w .. 32w + 31 x the 64
+// channels (two v_mfma_f32_32x32x16 accumulators).
+// Producer: thread (pixel p = tid / 2, half h = tid % 2) samples 16 channels of its pixel per
+// k-step: per tap it forms the 4 corner offsets and bilinear weights from the offset / mask conv
+// output (the om values of the next tap are loaded one tap ahead), per k-step it loads its 4 x 32 B
+// of corner data one step ahead, blends in fp32 in dcn_sample's exact order (sum of w_c * v_c,
+// then x mask, one rounding to T) and writes 32 B to the double-buffered LDS tile; the 64 x 32 weight
+// slice of the step is one 16-byte load per thread. One barrier per k-step: the MFMAs of step s
+// read buffer s & 1 while the producers fill buffer (s + 1) & 1.
+#include "conv_common.h"
+
+namespace tv {
+namespace dcn {
+
+constexpr int NT = 256, BMP = 128, BNC = 64, KS = 32;
+constexpr int PITCH = 80;                 // LDS row pitch (bytes): 64 B of K + 16 B pad, conflict-free
+constexpr int ABUF = BMP * PITCH;         // sampled pixels x 32 K
+constexpr int WBUF = BNC * PITCH;         // weight rows x 32 K
+constexpr int LDS = 2 * (ABUF + WBUF);
+
+template <typename T>
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  typedef T t2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, t2{(T)a, (T)b});
+}
+template <typename T>
+__device__ __forceinline__ float elem(const uint4& u, int i) {
+  const T* e = reinterpret_cast<const T*>(&u);
+  return (float)e[i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int HW = p.H * p.W;
+  const int M = p.B * HW;
+  const int m0 = blockIdx.x * BMP, n0 = blockIdx.y * BNC;
+  const int ncb = p.C / KS;
+  const int S = 9 * ncb;
+
+  // ---- producer geometry: pixel p, 16-channel half h
+  const int pp = tid >> 1, h = tid & 1;
+  const int m = m0 + pp;
+  const bool mval = m < M;
+  const int b = mval ? m / HW : 0;
+  const int rem = mval ? m - b * HW : 0;
+  const int oy = rem / p.W, ox = rem - (rem / p.W) * p.W;
+  const T* om = reinterpret_cast<const T*>(p.om) + (size_t)(mval ? m : 0) * p.om_ldc;
+  const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * HW * p.ldx + 16 * h;
+
+  // per-tap sampling state (dcn_sample's expressions)
+  int coff[4];
+  float wt[4], mask = 0.f;
+  auto tap_params = [&](int k, float dy, float dx, float logit) __attribute__((always_inline)) {
+    mask = 1.0f / (1.0f + expf(-logit));
+    const float py = (float)(oy - 1 + k / 3) + dy;
+    const float px = (float)(ox - 1 + k % 3) + dx;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) coff[c] = -1;
+    if (mval && py > -1.f && py < (float)p.H && px > -1.f && px < (float)p.W) {
+      const float fy = floorf(py), fx = floorf(px);
+      const int y0 = (int)fy, x0 = (int)fx;
+      const float ly = py - fy, lx = px - fx, hy = 1.f - ly, hx = 1.f - lx;
+      wt[0] = hy * hx;
+      wt[1] = hy * lx;
+      wt[2] = ly * hx;
+      wt[3] = ly * lx;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int yy = y0 + (c >> 1), xx = x0 + (c & 1);
+        if (yy >= 0 && yy <= p.H - 1 && xx >= 0 && xx <= p.W - 1) coff[c] = (yy * p.W + xx) * p.ldx;
+      }
+    }
+  };
+  // om values of tap k (loaded one tap ahead)
+  float nom[3];
+  auto load_om = [&](int k) __attribute__((always_inline)) {
+    nom[0] = (float)om[2 * k];
+    nom[1] = (float)om[2 * k + 1];
+    nom[2] = (float)om[18 + k];
+  };
+  // corner data of step s = (tap, cb): 4 corners x 2 x 16 B
+  uint4 cv[4][2];
+  auto load_corners = [&](int cb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const T* src = xb + (coff[c] < 0 ? 0 : coff[c]) + cb * KS;
+      cv[c][0] = coff[c] < 0 ? make_uint4(0, 0, 0, 0) : gload16(src);
+      cv[c][1] = coff[c] < 0 ? make_uint4(0, 0, 0, 0) : gload16(src + 8);
+    }
+  };
+  // weight slice of step s: row r = tid / 4, 16-byte chunk tid % 4
+  const int wr = tid >> 2, wc = tid & 3;
+  const T* wrow = reinterpret_cast<const T*>(p.w) + (size_t)(n0 + wr) * p.Kpad + 8 * wc;
+  uint4 wv;
+  auto load_w = [&](int s) __attribute__((always_inline)) {
+    const int k = s / ncb, cb = s - k * ncb;
+    wv = gload16(wrow + k * p.C + cb * KS);
+  };
+
+  auto produce = [&](int s) __attribute__((always_inline)) {
+    char* A = smem + (s & 1) * (ABUF + WBUF);
+    char* Wl = A + ABUF;
+    unsigned o[8];
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (coff[c] >= 0) {
+          a0 += wt[c] * elem<T>(cv[c][e >> 3], e & 7);
+          a1 += wt[c] * elem<T>(cv[c][e >> 3], (e & 7) + 1);
+        }
+      }
+      a0 *= mask;
+      a1 *= mask;
+      o[e >> 1] = pack2<T>(a0, a1);
+    }
+    *reinterpret_cast<uint4*>(A + pp * PITCH + 32 * h) = make_uint4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<uint4*>(A + pp * PITCH + 32 * h + 16) = make_uint4(o[4], o[5], o[6], o[7]);
+    *reinterpret_cast<uint4*>(Wl + wr * PITCH + 16 * wc) = wv;
+  };
+
+  f32x16 acc[2] = {f32x16{}, f32x16{}};
+  auto consume = [&](int s) __attribute__((always_inline)) {
+    const char* A = smem + (s & 1) * (ABUF + WBUF);
+    const char* Wl = A + ABUF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // two 16-deep sub-steps
+      const uint4 xf = *reinterpret_cast<const uint4*>(A + (32 * wave + l32) * PITCH + 32 * j + 16 * lh);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint4 wf = *reinterpret_cast<const uint4*>(Wl + (32 * i + l32) * PITCH + 32 * j + 16 * lh);
+        Mfma<T>::run(wf, xf, acc[i]);
+      }
+    }
+  };
+
+  // ---- pipeline: params of tap 0, om of tap 1, operands of step 0
+  load_om(0);
+  tap_params(0, nom[0], nom[1], nom[2]);
+  if (S > ncb) load_om(1);
+  load_corners(0);
+  load_w(0);
+  for (int s = 0; s < S; ++s) {
+    produce(s);  // blends step s's corners (loaded one step ahead) into LDS buffer s & 1
+    const int s1 = s + 1;
+    if (s1 < S) {
+      const int k1 = s1 / ncb, cb1 = s1 - k1 * ncb;
+      if (cb1 == 0) {  // a new tap: its sampling state from the om values loaded a tap ahead
+        tap_params(k1, nom[0], nom[1], nom[2]);
+        if (k1 + 1 < 9) load_om(k1 + 1);
+      }
+      load_corners(cb1);
+      load_w(s1);
+    }
+    __syncthreads();  // buffer s & 1 complete; every wave's reads of buffer (s - 1) & 1 are done
+    consume(s);
+  }
+
+  // ---- epilogue: channel rows (r & 3) + 8 (r >> 2) + 4 lh of block i, pixel column l32
+  const int mo = m0 + 32 * wave + l32;
+  if (mo >= M) return;
+  T* dst = reinterpret_cast<T*>(p.out) + (size_t)mo * p.out_ldc + n0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = 32 * i + 8 * g + 4 * lh;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc[i][4 * g + e] + p.bias[n0 + ch + e];
+        if (p.act == 1) t = fmaxf(t, 0.0f);
+        else if (p.act == 2) t = fmaxf(t, 0.01f * t);
+        v[e] = t;
+      }
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(dst + ch) = u32x2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+    }
+}
+
+}  // namespace dcn
+
+bool dcn_gemm_supported(int C, int N, int ldx, int om_ldc, int out_ldc) {
+  return C % dcn::KS == 0 && N % dcn::BNC == 0 && ldx % 8 == 0 && om_ldc >= 27 && out_ldc % 4 == 0;
+}
+
+int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s) {
+  if (!dcn_gemm_supported(p.C, p.N, p.ldx, p.om_ldc, p.out_ldc) || p.Kpad < 9 * p.C) {
+    set_error("dcn_gemm: channels must be multiples of 32 (input) / 64 (output)");
+    return 1;
+  }
+  const long M = (long)p.B * p.H * p.W;
+  dim3 grid((unsigned)((M + dcn::BMP - 1) / dcn::BMP), (unsigned)(p.N / dcn::BNC));
+  if (dtype == F16) {
+    hipLaunchKernelGGL(dcn::dcn_gemm<_Float16>, grid, dim3(dcn::NT), dcn::LDS, s, p);
+  } else if (dtype == BF16) {
+    hipLaunchKernelGGL(dcn::dcn_gemm<__bf16>, grid, dim3(dcn::NT), dcn::LDS, s, p);
+  } else {
+    set_error("dcn_gemm: fp16/bf16 only");
+    return 1;
+  }
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace tv

@@ -364,6 +364,13 @@ int Engine::make_workspace(int B, Workspace* ws) {
     for (const SegSpec& s : op.segs) last[s.src] = std::max(last[s.src], (int)i);
     if (op.src >= 0) last[op.src] = std::max(last[op.src], (int)i);
     if (op.add >= 0) last[op.add] = std::max(last[op.add], (int)i);
+    // the fused DCNv2 kernel (dcn.hip) samples x and reads the offset / mask tensor while it runs
+    // the column GEMM (op i): both stay live through it
+    if (op.kind == OP_CONV && i > 0 && plan.ops[i - 1].kind == OP_DCN && op.segs.size() == 1 &&
+        op.segs[0].src == plan.ops[i - 1].out) {
+      last[plan.ops[i - 1].src] = std::max(last[plan.ops[i - 1].src], (int)i);
+      last[plan.ops[i - 1].add] = std::max(last[plan.ops[i - 1].add], (int)i);
+    }
   }
   ws->off.assign(nt, 0);
   struct Live { size_t off, size; int last; };
@@ -608,6 +615,38 @@ int Engine::make_workspace(int B, Workspace* ws) {
       ws->use_pipe[i] = 0;
     }
   }
+  // DCNv2 sampling + its column GEMM -> one fused kernel (dcn.hip)
+  ws->dcn_skip.assign(plan.ops.size(), 0);
+  ws->dcn.assign(plan.ops.size(), DcnParams{});
+  for (size_t i = 0; dtype != F32 && i + 1 < plan.ops.size(); ++i) {
+    const OpSpec& d = plan.ops[i];
+    const OpSpec& g = plan.ops[i + 1];
+    if (d.kind != OP_DCN || g.kind != OP_CONV || g.segs.size() != 1 || g.segs[0].src != d.out ||
+        g.segs[0].row_expand != 9 || g.out < 0 || g.add >= 0)
+      continue;
+    const TensorSpec& xt = plan.tensors[d.src];
+    const TensorSpec& omt = plan.tensors[d.add];
+    const TensorSpec& ot = plan.tensors[g.out];
+    if (!dcn_gemm_supported(xt.C, g.N, xt.C, omt.C, ot.C) || g.segs[0].cin != xt.C) continue;
+    DcnParams& q = ws->dcn[i + 1];
+    q.x = base + ws->off[d.src];
+    q.B = B;
+    q.H = xt.H;
+    q.W = xt.W;
+    q.C = xt.C;
+    q.ldx = xt.C;
+    q.om = base + ws->off[d.add];
+    q.om_ldc = omt.C;
+    q.w = packed[i + 1].w;
+    q.Kpad = packed[i + 1].Kpad;
+    q.bias = packed[i + 1].bias;
+    q.act = g.act;
+    q.out = base + ws->off[g.out];
+    q.out_ldc = ot.C;
+    q.N = g.N;
+    ws->dcn_skip[i] = 1;
+    ws->use_pipe[i + 1] = 0;
+  }
   // stacked 3x3 heads on conv3x3 + block-diagonal 1x1 heads -> one launch (EPI 1)
   ws->head_fused.assign(plan.ops.size(), 0);
   ws->head_skip.assign(plan.ops.size(), 0);
@@ -739,6 +778,8 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     return input_u8 ? launch_prep_u8((const uint8_t*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s)
                     : launch_prep_nchw((const float*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s);
   }
+  if (ws->dcn_skip[i]) return TV_OK;  // sampled inside the next op's fused DCNv2 kernel
+  if (ws->dcn[i].x) return launch_dcn_gemm(ws->dcn[i], dtype, s);
   if (op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_DWCONVT_ADD) {
     const TensorSpec& src = plan.tensors[op.src];
     const TensorSpec& dst = plan.tensors[op.out];
@@ -903,13 +944,15 @@ const char* Engine::op_kernel(int B, size_t i) {
     const char* t = tn[dtype];
     const char* o = (op.out < 0) ? "float" : t;
     std::string& name = ws->kname[i];
-    if (name.empty() && (op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_DWCONVT_ADD))
+    if (name.empty() && !ws->dcn_skip[i] && (op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_DWCONVT_ADD))
       name = std::string(op.kind == OP_MAXPOOL ? "tv::dla::maxpool2_ceil<" : op.kind == OP_DCN ? "tv::dla::dcn_sample<"
                                                                                             : "tv::dla::dwconvt_add<") +
              t + ">";
     if (name.empty()) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
+      else if (ws->dcn_skip[i]) name = "(sampled inside the fused DCNv2 kernel)";
+      else if (ws->dcn[i].x) name = std::string("tv::dcn::dcn_gemm<") + t + ">";
       else if (ws->small[i])
         name = std::string("tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";

@@ -41,6 +41,8 @@ struct Workspace {
   std::vector<int> head_fused;      // per op: 1 = stacked 3x3 heads with the 1x1 heads fused in
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
   std::vector<int> small;           // per op: 1 = narrow-channel 3x3 conv on conv_small.hip
+  std::vector<int> dcn_skip;        // per op: 1 = DCN sampling done inside the next op's fused kernel
+  std::vector<DcnParams> dcn;       // per op: fused DCNv2 launch (dcn.hip) when dcn[i].x != null
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
   std::vector<ConvTParams> tparams; // per op: convt.hip launch parameters
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops

@@ -126,7 +126,7 @@ struct DcnParams {
   void* out;          // [B, H, W, out_ldc], N channels
   int out_ldc, N;
 };
-bool dcn_gemm_supported(int C, int N, int ldx, int om_ldc, int out_ldc);
+bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad);
 int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s);
 
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->

@@ -11,11 +11,14 @@
 // Producer: thread (pixel p = tid / 2, half h = tid % 2) samples 16 channels of its pixel per
 // k-step: per tap it forms the 4 corner offsets and bilinear weights from the offset / mask conv
 // output (the om values of the next tap are loaded one tap ahead), per k-step it loads its 4 x 32 B
-// of corner data one step ahead, blends in fp32 in dcn_sample's exact order (sum of w_c * v_c,
-// then x mask, one rounding to T) and writes 32 B to the double-buffered LDS tile; the 64 x 32 weight
+// of corner data one step ahead (buffer loads: invalid corners read as zero), blends in fp32 as
+// sum of (w_c * mask) * v_c with one rounding to T (dcn_sample multiplies by the mask after the
+// corner sum: the same value up to fp32 rounding) and writes 32 B to the double-buffered LDS tile; the 64 x 32 weight
 // slice of the step is one 16-byte load per thread. One barrier per k-step: the MFMAs of step s
 // read buffer s & 1 while the producers fill buffer (s + 1) & 1.
 #include "conv_common.h"
+
+#include <type_traits>
 
 namespace tv {
 namespace dcn {
@@ -25,11 +28,37 @@ constexpr int PITCH = 80;                 // LDS row pitch (bytes): 64 B of K + 
 constexpr int ABUF = BMP * PITCH;         // sampled pixels x 32 K
 constexpr int WBUF = BNC * PITCH;         // weight rows x 32 K
 constexpr int LDS = 2 * (ABUF + WBUF);
+constexpr int kOOB = 0x7ff00000;          // buffer offset past any num_records (host checks the sizes)
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ __forceinline__ uint4 to_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
 template <typename T>
 __device__ __forceinline__ unsigned pack2(float a, float b) {
   typedef T t2 __attribute__((ext_vector_type(2)));
   return __builtin_bit_cast(unsigned, t2{(T)a, (T)b});
+}
+// w * f16 (low / high half of v) [+ acc] in fp32
+__device__ __forceinline__ float mix_lo(float w, unsigned v) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel_hi:[0,1,0]" : "=v"(r) : "v"(w), "v"(v));
+  return r;
+}
+__device__ __forceinline__ float mix_hi(float w, unsigned v) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, 0 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(r) : "v"(w), "v"(v));
+  return r;
+}
+__device__ __forceinline__ float mix_lo_acc(float w, unsigned v, float acc) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(r) : "v"(w), "v"(v), "v"(acc));
+  return r;
+}
+__device__ __forceinline__ float mix_hi_acc(float w, unsigned v, float acc) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(r) : "v"(w), "v"(v), "v"(acc));
+  return r;
 }
 template <typename T>
 __device__ __forceinline__ float elem(const uint4& u, int i) {
@@ -56,29 +85,43 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
   const int rem = mval ? m - b * HW : 0;
   const int oy = rem / p.W, ox = rem - (rem / p.W) * p.W;
   const T* om = reinterpret_cast<const T*>(p.om) + (size_t)(mval ? m : 0) * p.om_ldc;
-  const T* xb = reinterpret_cast<const T*>(p.x) + (size_t)b * HW * p.ldx + 16 * h;
 
-  // per-tap sampling state (dcn_sample's expressions)
-  int coff[4];
-  float wt[4], mask = 0.f;
+  // x and the weights through buffer resources: per tap, one byte offset per corner (an invalid
+  // corner's offset lies past num_records, so its load returns zeros and the blend needs no
+  // select), the channel block / k-step in the scalar offset
+  i32x4 xr, wrs;
+  {
+    const unsigned long long a = (unsigned long long)p.x, aw = (unsigned long long)p.w;
+    xr = i32x4{(int)(unsigned)a, (int)(unsigned)(a >> 32), (int)((unsigned)M * p.ldx * (unsigned)sizeof(T)), 0x00020000};
+    wrs = i32x4{(int)(unsigned)aw, (int)(unsigned)(aw >> 32), (int)((unsigned)p.N * p.Kpad * (unsigned)sizeof(T)),
+                0x00020000};
+  }
+  const int xlane = (b * HW * p.ldx + 16 * h) * (int)sizeof(T);
+
+  // per-tap sampling state (dcn_sample's expressions; the mask is folded into the corner weights)
+  int voff[4];
+  float wt[4];
   auto tap_params = [&](int k, float dy, float dx, float logit) __attribute__((always_inline)) {
-    mask = 1.0f / (1.0f + expf(-logit));
+    const float mask = 1.0f / (1.0f + expf(-logit));
     const float py = (float)(oy - 1 + k / 3) + dy;
     const float px = (float)(ox - 1 + k % 3) + dx;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) coff[c] = -1;
+    for (int c = 0; c < 4; ++c) {
+      voff[c] = kOOB;
+      wt[c] = 0.f;
+    }
     if (mval && py > -1.f && py < (float)p.H && px > -1.f && px < (float)p.W) {
       const float fy = floorf(py), fx = floorf(px);
       const int y0 = (int)fy, x0 = (int)fx;
       const float ly = py - fy, lx = px - fx, hy = 1.f - ly, hx = 1.f - lx;
-      wt[0] = hy * hx;
-      wt[1] = hy * lx;
-      wt[2] = ly * hx;
-      wt[3] = ly * lx;
+      const float w4[4] = {hy * hx, hy * lx, ly * hx, ly * lx};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int yy = y0 + (c >> 1), xx = x0 + (c & 1);
-        if (yy >= 0 && yy <= p.H - 1 && xx >= 0 && xx <= p.W - 1) coff[c] = (yy * p.W + xx) * p.ldx;
+        if (yy >= 0 && yy <= p.H - 1 && xx >= 0 && xx <= p.W - 1) {
+          voff[c] = xlane + (yy * p.W + xx) * p.ldx * (int)sizeof(T);
+          wt[c] = w4[c] * mask;
+        }
       }
     }
   };
@@ -94,18 +137,16 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
   auto load_corners = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const T* src = xb + (coff[c] < 0 ? 0 : coff[c]) + cb * KS;
-      cv[c][0] = coff[c] < 0 ? make_uint4(0, 0, 0, 0) : gload16(src);
-      cv[c][1] = coff[c] < 0 ? make_uint4(0, 0, 0, 0) : gload16(src + 8);
+      cv[c][0] = to_u4(raw_buffer_load_v4(xr, voff[c], cb * KS * (int)sizeof(T), 0));
+      cv[c][1] = to_u4(raw_buffer_load_v4(xr, voff[c], cb * KS * (int)sizeof(T) + 16, 0));
     }
   };
-  // weight slice of step s: row r = tid / 4, 16-byte chunk tid % 4
+  // weight slice of step s: row r = tid / 4, 16-byte chunk tid % 4 (K = tap * C + cb * 32 = 32 s)
   const int wr = tid >> 2, wc = tid & 3;
-  const T* wrow = reinterpret_cast<const T*>(p.w) + (size_t)(n0 + wr) * p.Kpad + 8 * wc;
+  const int wvoff = ((n0 + wr) * p.Kpad + 8 * wc) * (int)sizeof(T);
   uint4 wv;
   auto load_w = [&](int s) __attribute__((always_inline)) {
-    const int k = s / ncb, cb = s - k * ncb;
-    wv = gload16(wrow + k * p.C + cb * KS);
+    wv = to_u4(raw_buffer_load_v4(wrs, wvoff, s * KS * (int)sizeof(T), 0));
   };
 
   auto produce = [&](int s) __attribute__((always_inline)) {
@@ -114,16 +155,28 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
     unsigned o[8];
 #pragma unroll
     for (int e = 0; e < 16; e += 2) {
-      float a0 = 0.f, a1 = 0.f;
+      float a0, a1;
+      if constexpr (std::is_same<T, _Float16>::value) {
+        // v_fma_mix reads the f16 halves in place (op_sel picks the high one): one VALU op per
+        // element and corner
+        const unsigned* d0 = reinterpret_cast<const unsigned*>(&cv[0][e >> 3]);
+        a0 = mix_lo(wt[0], d0[(e & 7) >> 1]);
+        a1 = mix_hi(wt[0], d0[(e & 7) >> 1]);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (coff[c] >= 0) {
+        for (int c = 1; c < 4; ++c) {
+          const unsigned dw = reinterpret_cast<const unsigned*>(&cv[c][e >> 3])[(e & 7) >> 1];
+          a0 = mix_lo_acc(wt[c], dw, a0);
+          a1 = mix_hi_acc(wt[c], dw, a1);
+        }
+      } else {
+        a0 = 0.f;
+        a1 = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
           a0 += wt[c] * elem<T>(cv[c][e >> 3], e & 7);
           a1 += wt[c] * elem<T>(cv[c][e >> 3], (e & 7) + 1);
         }
       }
-      a0 *= mask;
-      a1 *= mask;
       o[e >> 1] = pack2<T>(a0, a1);
     }
     *reinterpret_cast<uint4*>(A + pp * PITCH + 32 * h) = make_uint4(o[0], o[1], o[2], o[3]);
@@ -192,13 +245,15 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
 
 }  // namespace dcn
 
-bool dcn_gemm_supported(int C, int N, int ldx, int om_ldc, int out_ldc) {
+bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad) {
+  // buffer offsets are 32-bit: the input and weight tensors stay below the out-of-range marker
+  if (M * ldx * 2 >= dcn::kOOB || (long)N * Kpad * 2 >= dcn::kOOB) return false;
   return C % dcn::KS == 0 && N % dcn::BNC == 0 && ldx % 8 == 0 && om_ldc >= 27 && out_ldc % 4 == 0;
 }
 
 int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s) {
-  if (!dcn_gemm_supported(p.C, p.N, p.ldx, p.om_ldc, p.out_ldc) || p.Kpad < 9 * p.C) {
-    set_error("dcn_gemm: channels must be multiples of 32 (input) / 64 (output)");
+  if (!dcn_gemm_supported((long)p.B * p.H * p.W, p.C, p.N, p.ldx, p.om_ldc, p.out_ldc, p.Kpad) || p.Kpad < 9 * p.C) {
+    set_error("dcn_gemm: channels must be multiples of 32 (input) / 64 (output), tensors below 2 GB");
     return 1;
   }
   const long M = (long)p.B * p.H * p.W;

@@ -627,7 +627,9 @@ int Engine::make_workspace(int B, Workspace* ws) {
     const TensorSpec& xt = plan.tensors[d.src];
     const TensorSpec& omt = plan.tensors[d.add];
     const TensorSpec& ot = plan.tensors[g.out];
-    if (!dcn_gemm_supported(xt.C, g.N, xt.C, omt.C, ot.C) || g.segs[0].cin != xt.C) continue;
+    if (!dcn_gemm_supported((long)B * xt.H * xt.W, xt.C, g.N, xt.C, omt.C, ot.C, packed[i + 1].Kpad) ||
+        g.segs[0].cin != xt.C)
+      continue;
     DcnParams& q = ws->dcn[i + 1];
     q.x = base + ws->off[d.src];
     q.B = B;

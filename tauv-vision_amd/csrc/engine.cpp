@@ -954,7 +954,7 @@ const char* Engine::op_kernel(int B, size_t i) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->dcn_skip[i]) name = "(sampled inside the fused DCNv2 kernel)";
-      else if (ws->dcn[i].x) name = std::string("tv::dcn::dcn_gemm<") + t + ">";
+      else if (ws->dcn[i].x) name = std::string("tv::dcn::dcn_gemm<") + t + (ws->dcn[i].N % 128 == 0 ? ", 128>" : ", 64>");
       else if (ws->small[i])
         name = std::string("tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";

@@ -4,18 +4,17 @@
 // tensor in HBM (dcn_sample + an implicit GEMM over the columns moved 2 x 9C x 2 B per pixel: 1.4 GB
 // per 64-channel layer at 32 frames of 120x160).
 //
-// GEMM view: rows = BN output channels (A = the DeformConv2d weight, BN folded, K = tap * C + c as
+// GEMM view: rows = 64 output channels (A = the DeformConv2d weight, BN folded, K = tap * C + c as
 // the column GEMM packs it), columns = 128 output pixels (B = the sampled values), K in steps of 32
-// (one tap, 32 channels). Workgroup = 4 waves; wave w owns pixels 32w .. 32w + 31 x the BN
-// channels (BN / 32 v_mfma_f32_32x32x16 accumulators).
+// (one tap, 32 channels). Workgroup = 4 waves; wave w owns pixels 32w .. 32w + 31 x the 64
+// channels (two v_mfma_f32_32x32x16 accumulators).
 // Producer: thread (pixel p = tid / 2, half h = tid % 2) samples 16 channels of its pixel per
 // k-step: per tap it forms the 4 corner offsets and bilinear weights from the offset / mask conv
 // output (the om values of the next tap are loaded one tap ahead), per k-step it loads its 4 x 32 B
 // of corner data one step ahead (buffer loads: invalid corners read as zero), blends in fp32 as
 // sum of (w_c * mask) * v_c with one rounding to T (dcn_sample multiplies by the mask after the
-// corner sum: the same value up to fp32 rounding) and writes 32 B to the double-buffered LDS
-// tile; the BN x 32 weight slice of the step is BN / 64 16-byte loads per thread (BN = 128 output
-// channels when N allows, so one sampled tile feeds 8 MFMAs per wave, else 64). One barrier per k-step: the MFMAs of step s
+// corner sum: the same value up to fp32 rounding) and writes 32 B to the double-buffered LDS tile; the 64 x 32 weight
+// slice of the step is one 16-byte load per thread. One barrier per k-step: the MFMAs of step s
 // read buffer s & 1 while the producers fill buffer (s + 1) & 1.
 #include "conv_common.h"
 
@@ -24,11 +23,11 @@
 namespace tv {
 namespace dcn {
 
-constexpr int NT = 256, BMP = 128, KS = 32;
+constexpr int NT = 256, BMP = 128, BNC = 64, KS = 32;
 constexpr int PITCH = 80;                 // LDS row pitch (bytes): 64 B of K + 16 B pad, conflict-free
 constexpr int ABUF = BMP * PITCH;         // sampled pixels x 32 K
-template <int BN> constexpr int wbuf() { return BN * PITCH; }  // weight rows x 32 K
-template <int BN> constexpr int lds_bytes() { return 2 * (ABUF + wbuf<BN>()); }
+constexpr int WBUF = BNC * PITCH;         // weight rows x 32 K
+constexpr int LDS = 2 * (ABUF + WBUF);
 constexpr int kOOB = 0x7ff00000;          // buffer offset past any num_records (host checks the sizes)
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -67,21 +66,14 @@ __device__ __forceinline__ float elem(const uint4& u, int i) {
   return (float)e[i];
 }
 
-template <typename T, int BN>
+template <typename T>
 __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
-  constexpr int NA = BN / 32;  // 32-channel accumulator blocks per wave
-  constexpr int WBUF = wbuf<BN>();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, lh = lane >> 5;
   const int HW = p.H * p.W;
   const int M = p.B * HW;
-  // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a contiguous range of pixel tiles
-  // (its L2 then holds the rows those tiles' corners read) and keep the output-channel blocks of a
-  // tile adjacent in time
-  const int G = gridDim.x, ny = p.N / BN;
-  const int q = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const int m0 = (q / ny) * BMP, n0 = (q % ny) * BN;
+  const int m0 = blockIdx.x * BMP, n0 = blockIdx.y * BNC;
   const int ncb = p.C / KS;
   const int S = 9 * ncb;
 
@@ -108,7 +100,12 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
 
   // per-tap sampling state (dcn_sample's expressions; the mask is folded into the corner weights)
   int voff[4];
-  float wt[4];
+  float wt[4];  // the tap being issued
+  struct Set {
+    uint4 cv[4][2];
+    uint4 wv;
+    float wt[4];
+  };
   auto tap_params = [&](int k, float dy, float dx, float logit) __attribute__((always_inline)) {
     const float mask = 1.0f / (1.0f + expf(-logit));
     const float py = (float)(oy - 1 + k / 3) + dy;
@@ -140,26 +137,25 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
     nom[1] = (float)om[2 * k + 1];
     nom[2] = (float)om[18 + k];
   };
-  // corner data of step s = (tap, cb): 4 corners x 2 x 16 B
-  uint4 cv[4][2];
-  auto load_corners = [&](int cb) __attribute__((always_inline)) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      cv[c][0] = to_u4(raw_buffer_load_v4(xr, voff[c], cb * KS * (int)sizeof(T), 0));
-      cv[c][1] = to_u4(raw_buffer_load_v4(xr, voff[c], cb * KS * (int)sizeof(T) + 16, 0));
-    }
-  };
-  // weight slice of step s: row r = tid / 4, 16-byte chunk tid % 4 (K = tap * C + cb * 32 = 32 s)
   const int wr = tid >> 2, wc = tid & 3;
   const int wvoff = ((n0 + wr) * p.Kpad + 8 * wc) * (int)sizeof(T);
-  uint4 wv[BN / 64];  // rows wr, wr + 64
-  auto load_w = [&](int s) __attribute__((always_inline)) {
+  // step s = (tap, cb) into a register set: 4 corners x 2 x 16 B + the weight chunk
+  auto issue = [&](int s, Set& st) __attribute__((always_inline)) {
+    const int k = s / ncb, cb = s - k * ncb;
+    if (cb == 0) {
+      tap_params(k, nom[0], nom[1], nom[2]);
+      if (k + 1 < 9) load_om(k + 1);
+    }
 #pragma unroll
-    for (int j = 0; j < BN / 64; ++j)
-      wv[j] = to_u4(raw_buffer_load_v4(wrs, wvoff + j * 64 * p.Kpad * (int)sizeof(T), s * KS * (int)sizeof(T), 0));
+    for (int c = 0; c < 4; ++c) {
+      st.wt[c] = wt[c];
+      st.cv[c][0] = to_u4(raw_buffer_load_v4(xr, voff[c], cb * KS * (int)sizeof(T), 0));
+      st.cv[c][1] = to_u4(raw_buffer_load_v4(xr, voff[c], cb * KS * (int)sizeof(T) + 16, 0));
+    }
+    st.wv = to_u4(raw_buffer_load_v4(wrs, wvoff, s * KS * (int)sizeof(T), 0));
   };
 
-  auto produce = [&](int s) __attribute__((always_inline)) {
+  auto produce = [&](int s, const Set& st) __attribute__((always_inline)) {
     char* A = smem + (s & 1) * (ABUF + WBUF);
     char* Wl = A + ABUF;
     unsigned o[8];
@@ -169,35 +165,32 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
       if constexpr (std::is_same<T, _Float16>::value) {
         // v_fma_mix reads the f16 halves in place (op_sel picks the high one): one VALU op per
         // element and corner
-        const unsigned* d0 = reinterpret_cast<const unsigned*>(&cv[0][e >> 3]);
-        a0 = mix_lo(wt[0], d0[(e & 7) >> 1]);
-        a1 = mix_hi(wt[0], d0[(e & 7) >> 1]);
+        const unsigned* d0 = reinterpret_cast<const unsigned*>(&st.cv[0][e >> 3]);
+        a0 = mix_lo(st.wt[0], d0[(e & 7) >> 1]);
+        a1 = mix_hi(st.wt[0], d0[(e & 7) >> 1]);
 #pragma unroll
         for (int c = 1; c < 4; ++c) {
-          const unsigned dw = reinterpret_cast<const unsigned*>(&cv[c][e >> 3])[(e & 7) >> 1];
-          a0 = mix_lo_acc(wt[c], dw, a0);
-          a1 = mix_hi_acc(wt[c], dw, a1);
+          const unsigned dw = reinterpret_cast<const unsigned*>(&st.cv[c][e >> 3])[(e & 7) >> 1];
+          a0 = mix_lo_acc(st.wt[c], dw, a0);
+          a1 = mix_hi_acc(st.wt[c], dw, a1);
         }
       } else {
         a0 = 0.f;
         a1 = 0.f;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          a0 += wt[c] * elem<T>(cv[c][e >> 3], e & 7);
-          a1 += wt[c] * elem<T>(cv[c][e >> 3], (e & 7) + 1);
+          a0 += st.wt[c] * elem<T>(st.cv[c][e >> 3], e & 7);
+          a1 += st.wt[c] * elem<T>(st.cv[c][e >> 3], (e & 7) + 1);
         }
       }
       o[e >> 1] = pack2<T>(a0, a1);
     }
     *reinterpret_cast<uint4*>(A + pp * PITCH + 32 * h) = make_uint4(o[0], o[1], o[2], o[3]);
     *reinterpret_cast<uint4*>(A + pp * PITCH + 32 * h + 16) = make_uint4(o[4], o[5], o[6], o[7]);
-#pragma unroll
-    for (int j = 0; j < BN / 64; ++j) *reinterpret_cast<uint4*>(Wl + (wr + 64 * j) * PITCH + 16 * wc) = wv[j];
+    *reinterpret_cast<uint4*>(Wl + wr * PITCH + 16 * wc) = st.wv;
   };
 
-  f32x16 acc[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) acc[i] = f32x16{};
+  f32x16 acc[2] = {f32x16{}, f32x16{}};
   auto consume = [&](int s) __attribute__((always_inline)) {
     const char* A = smem + (s & 1) * (ABUF + WBUF);
     const char* Wl = A + ABUF;
@@ -205,33 +198,27 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
     for (int j = 0; j < 2; ++j) {  // two 16-deep sub-steps
       const uint4 xf = *reinterpret_cast<const uint4*>(A + (32 * wave + l32) * PITCH + 32 * j + 16 * lh);
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
+      for (int i = 0; i < 2; ++i) {
         const uint4 wf = *reinterpret_cast<const uint4*>(Wl + (32 * i + l32) * PITCH + 32 * j + 16 * lh);
         Mfma<T>::run(wf, xf, acc[i]);
       }
     }
   };
 
-  // ---- pipeline: params of tap 0, om of tap 1, operands of step 0
+  // ---- pipeline (S = 9 * ncb is even): step s's operands in set s & 1, issued two steps ahead
+  Set st0, st1;
   load_om(0);
-  tap_params(0, nom[0], nom[1], nom[2]);
-  if (S > ncb) load_om(1);
-  load_corners(0);
-  load_w(0);
-  for (int s = 0; s < S; ++s) {
-    produce(s);  // blends step s's corners (loaded one step ahead) into LDS buffer s & 1
-    const int s1 = s + 1;
-    if (s1 < S) {
-      const int k1 = s1 / ncb, cb1 = s1 - k1 * ncb;
-      if (cb1 == 0) {  // a new tap: its sampling state from the om values loaded a tap ahead
-        tap_params(k1, nom[0], nom[1], nom[2]);
-        if (k1 + 1 < 9) load_om(k1 + 1);
-      }
-      load_corners(cb1);
-      load_w(s1);
-    }
-    __syncthreads();  // buffer s & 1 complete; every wave's reads of buffer (s - 1) & 1 are done
+  issue(0, st0);
+  issue(1, st1);
+  for (int s = 0; s < S; s += 2) {
+    produce(s, st0);
+    if (s + 2 < S) issue(s + 2, st0);
+    __syncthreads();
     consume(s);
+    produce(s + 1, st1);
+    if (s + 3 < S) issue(s + 3, st1);
+    __syncthreads();
+    consume(s + 1);
   }
 
   // ---- epilogue: channel rows (r & 3) + 8 (r >> 2) + 4 lh of block i, pixel column l32
@@ -239,7 +226,7 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
   if (mo >= M) return;
   T* dst = reinterpret_cast<T*>(p.out) + (size_t)mo * p.out_ldc + n0;
 #pragma unroll
-  for (int i = 0; i < NA; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int ch = 32 * i + 8 * g + 4 * lh;
@@ -261,7 +248,7 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad) {
   // buffer offsets are 32-bit: the input and weight tensors stay below the out-of-range marker
   if (M * ldx * 2 >= dcn::kOOB || (long)N * Kpad * 2 >= dcn::kOOB) return false;
-  return C % dcn::KS == 0 && N % 64 == 0 && ldx % 8 == 0 && om_ldc >= 27 && out_ldc % 4 == 0;
+  return C % (2 * dcn::KS) == 0 && N % dcn::BNC == 0 && ldx % 8 == 0 && om_ldc >= 27 && out_ldc % 4 == 0;
 }
 
 int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s) {
@@ -270,19 +257,14 @@ int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s) {
     return 1;
   }
   const long M = (long)p.B * p.H * p.W;
-  // 128 output channels per workgroup when N allows: each sampled tile feeds twice the MFMAs
-  const bool wide = p.N % 128 == 0;
-  dim3 grid((unsigned)((M + dcn::BMP - 1) / dcn::BMP * (p.N / (wide ? 128 : 64))));
-  if (dtype != F16 && dtype != BF16) {
+  dim3 grid((unsigned)((M + dcn::BMP - 1) / dcn::BMP), (unsigned)(p.N / dcn::BNC));
+  if (dtype == F16) {
+    hipLaunchKernelGGL(dcn::dcn_gemm<_Float16>, grid, dim3(dcn::NT), dcn::LDS, s, p);
+  } else if (dtype == BF16) {
+    hipLaunchKernelGGL(dcn::dcn_gemm<__bf16>, grid, dim3(dcn::NT), dcn::LDS, s, p);
+  } else {
     set_error("dcn_gemm: fp16/bf16 only");
     return 1;
-  }
-  if (dtype == F16) {
-    if (wide) hipLaunchKernelGGL((dcn::dcn_gemm<_Float16, 128>), grid, dim3(dcn::NT), dcn::lds_bytes<128>(), s, p);
-    else hipLaunchKernelGGL((dcn::dcn_gemm<_Float16, 64>), grid, dim3(dcn::NT), dcn::lds_bytes<64>(), s, p);
-  } else {
-    if (wide) hipLaunchKernelGGL((dcn::dcn_gemm<__bf16, 128>), grid, dim3(dcn::NT), dcn::lds_bytes<128>(), s, p);
-    else hipLaunchKernelGGL((dcn::dcn_gemm<__bf16, 64>), grid, dim3(dcn::NT), dcn::lds_bytes<64>(), s, p);
   }
   TV_HIP(hipGetLastError());
   return 0;

@@ -1,5 +1,5 @@
 """Profiling driver: N forwards of the bench workload (R18, 640x480, fp16) for rocprofv3
-kernel traces / PMC passes. Usage: python tools/prof_forward.py [--batch 64] [--iters 3]"""
+kernel traces / PMC passes. Usage: python tools/prof_forward.py [--batch 64] [--iters 3] [--model dla34]"""
 import argparse
 import os
 import sys
@@ -18,9 +18,10 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--precision", default="fp16")
+    ap.add_argument("--model", default="r18")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    model, oc, sd = build_model(a.precision, dev)
+    model, oc, sd = build_model(a.precision, dev, a.model)
     frames = torch.randint(0, 256, (a.batch, 480, 640, 3), device=dev, dtype=torch.uint8)
     eng = model.engine(dev, 480, 640)
     out = eng.alloc_out(a.batch)

@@ -13,6 +13,19 @@ inline int dtype_size(int dt) { return dt == F32 ? 4 : 2; }
 // Thread-local error string behind tv_last_error().
 void set_error(const std::string& msg);
 
+// Raise kernel K's dynamic-LDS limit to `bytes` once per process. The function-local static is
+// initialised under the C++ static-init guard, so concurrent first launches from several threads
+// (engines on side streams, callers' threads) set it exactly once; a failure is sticky.
+template <auto K>
+inline int ensure_lds(int bytes) {
+  static const hipError_t e = hipFuncSetAttribute((const void*)K, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess) {
+    set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
+    return 3;
+  }
+  return 0;
+}
+
 #define TV_HIP(expr)                                                                    \
   do {                                                                                  \
     hipError_t _e = (expr);                                                             \

@@ -229,15 +229,7 @@ __global__ __launch_bounds__(kThreads, 2) void conv_igemm(const ConvParams* __re
 template <typename T, typename OutT, int MODE>
 static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, hipStream_t s) {
   auto k = conv_igemm<T, OutT, MODE>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
-    if (e != hipSuccess) {
-      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-      return 3;
-    }
-    attr = true;
-  }
+  if (int r = ensure_lds<conv_igemm<T, OutT, MODE>>(kLdsBytes)) return r;
   dim3 grid(p.mtiles * p.ntiles);
   hipLaunchKernelGGL(k, grid, dim3(kThreads), kLdsBytes, s, dp, out);
   TV_HIP(hipGetLastError());

@@ -651,15 +651,7 @@ template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4, int
 inline int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
   auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>;
   constexpr int lds = lds_bytes<RES>();
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) {
-      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-      return 3;
-    }
-    attr = true;
-  }
+  if (int r = ensure_lds<conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>>(lds)) return r;
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, out);
   TV_HIP(hipGetLastError());
   return 0;

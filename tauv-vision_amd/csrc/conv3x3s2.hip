@@ -471,15 +471,7 @@ __global__ void repack_weights_s2(const uint4* __restrict__ w, int kpad16, uint4
 template <typename T, int ACT>
 static int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
   auto k = conv3x3s2<T, ACT>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) {
-      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-      return 3;
-    }
-    attr = true;
-  }
+  if (int r = ensure_lds<conv3x3s2<T, ACT>>(LDS)) return r;
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), LDS, s, dp, out);
   TV_HIP(hipGetLastError());
   return 0;

@@ -330,15 +330,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
 template <typename T, typename OutT, int MODE>
 static int launch_pipe_t(const ConvParams& p, const ConvParams* dp, void* out, hipStream_t s) {
   auto k = conv_pipe<T, OutT, MODE>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) {
-      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-      return 3;
-    }
-    attr = true;
-  }
+  if (int r = ensure_lds<conv_pipe<T, OutT, MODE>>(LDS)) return r;
   hipLaunchKernelGGL(k, dim3(p.mtiles * p.ntiles), dim3(NT), LDS, s, dp, out);
   TV_HIP(hipGetLastError());
   return 0;

@@ -133,51 +133,55 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto compute_store = [&](int t, int ph, const XSet& X, const ASet& A) __attribute__((always_inline)) {
     const char* wl = smem + ph * PW + l32 * WPITCH + lh * 16;
     const float* lb = reinterpret_cast<const float*>(smem + NP * PW) + ph * C;
-    f32x16 acc[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
-    // weight fragments one k-step at a time (bounded live set)
-#pragma unroll
-    for (int j = 0; j < KJ; ++j) {
-      uint4 wv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) wv[i] = *reinterpret_cast<const uint4*>(wl + i * 32 * WPITCH + j * 32);
-      {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Mfma<T>::run(wv[i], X.x[j], acc[i]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
     const long long tg = target(t, ph);
     T* out = reinterpret_cast<T*>(p.out) + (tg < 0 ? 0 : tg) * p.out_ldc;
+    // two halves of 64 output channels: half the accumulators live at a time (the x operand is
+    // reused, the weights are re-read from LDS) — keeps the kernel inside 256 VGPRs without spills
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int hf = 0; hf < 2; ++hf) {
+      f32x16 acc[2];
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        float v[2][4];
+      for (int i = 0; i < 2; ++i) acc[i] = f32x16{};
 #pragma unroll
-        for (int gg = 0; gg < 2; ++gg) {
-          const int G2 = 2 * m + gg;
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(lb + 32 * i + 8 * G2 + 4 * lh);
+      for (int j = 0; j < KJ; ++j) {
+        uint4 wv[2];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[gg][e] = acc[i][4 * G2 + e] + bb[e];
-        }
-        // registers -> 16-byte chunk: lanes 0-31 channels 32i+16m+0..7, lanes 32-63 +8..15
-        float f[8];
+        for (int i = 0; i < 2; ++i) wv[i] = *reinterpret_cast<const uint4*>(wl + (2 * hf + i) * 32 * WPITCH + j * 32);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][e]), __float_as_uint(v[1][e]), false,
-                                                          false);
-          f[e] = __uint_as_float(r[0]);
-          f[4 + e] = __uint_as_float(r[1]);
-        }
-        unsigned o[4];
-        const uint4 sk = A.a[2 * i + m];
-        const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = pack2<T>(lo_f<T>(sw[e]) + f[2 * e], hi_f<T>(sw[e]) + f[2 * e + 1]);
-        if (tg >= 0) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
+        for (int i = 0; i < 2; ++i) Mfma<T>::run(wv[i], X.x[j], acc[i]);
+        __builtin_amdgcn_sched_barrier(0);
       }
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        const int i = 2 * hf + ii;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          float v[2][4];
+#pragma unroll
+          for (int gg = 0; gg < 2; ++gg) {
+            const int G2 = 2 * m + gg;
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(lb + 32 * i + 8 * G2 + 4 * lh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[gg][e] = acc[ii][4 * G2 + e] + bb[e];
+          }
+          // registers -> 16-byte chunk: lanes 0-31 channels 32i+16m+0..7, lanes 32-63 +8..15
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0][e]), __float_as_uint(v[1][e]), false,
+                                                            false);
+            f[e] = __uint_as_float(r[0]);
+            f[4 + e] = __uint_as_float(r[1]);
+          }
+          unsigned o[4];
+          const uint4 sk = A.a[2 * i + m];
+          const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] = pack2<T>(lo_f<T>(sw[e]) + f[2 * e], hi_f<T>(sw[e]) + f[2 * e + 1]);
+          if (tg >= 0) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
+        }
+      }
+    }
   };
 
   // Steps (tile, phase) in order; the operands of the next step are loaded before the current
@@ -232,15 +236,7 @@ template <typename T, int NP>
 static int launch_t(const ConvTParams& p, hipStream_t s) {
   auto k = convt_add<T, NP>;
   constexpr int lds = lds_bytes<NP>();
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) {
-      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-      return 3;
-    }
-    attr = true;
-  }
+  if (int r = ensure_lds<convt_add<T, NP>>(lds)) return r;
   const int groups = p.s * p.s / NP;
   hipLaunchKernelGGL(k, dim3(groups * p.nchunks), dim3(NT), lds, s, p);
   TV_HIP(hipGetLastError());

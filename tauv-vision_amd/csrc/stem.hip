@@ -301,15 +301,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 template <typename T, int MODE>
 static int launch_t(const StemParams& p, int grid, hipStream_t s) {
   auto k = stem_conv<T, MODE>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    if (e != hipSuccess) {
-      set_error(std::string("hipFuncSetAttribute: ") + hipGetErrorString(e));
-      return 3;
-    }
-    attr = true;
-  }
+  if (int r = ensure_lds<stem_conv<T, MODE>>(LDS)) return r;
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), LDS, s, p);
   TV_HIP(hipGetLastError());
   return 0;

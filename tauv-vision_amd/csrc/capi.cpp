@@ -294,7 +294,7 @@ int tv_yolact_assemble_masks_indexed(const float* proto, const int64_t pst[4], i
 
 int tv_decode_workspace_size(int32_t B, int32_t C, int32_t H, int32_t W, int32_t K, int64_t* bytes) {
   if (!bytes || B < 1 || C < 1 || H < 1 || W < 1 || K < 1) { set_error("bad argument"); return TV_EINVAL; }
-  *bytes = (int64_t)select_workspace_bytes(B, C, H, W, K);
+  *bytes = (int64_t)decode_workspace_bytes(B, C, H, W, K);
   return TV_OK;
 }
 
@@ -336,7 +336,7 @@ int tv_decode(const float* heat, const int64_t hs[4], const float* size, const i
     }
     p.records = records;
     p.counts = counts;
-    return launch_select(heat, hs, B, C, H, W, 1, 1, K, ws, (size_t)ws_bytes, nullptr, nullptr, &p, s);
+    return launch_decode(heat, hs, B, C, H, W, K, ws, (size_t)ws_bytes, p, s);
   })
 }
 

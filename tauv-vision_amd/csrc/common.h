@@ -249,6 +249,11 @@ size_t select_workspace_bytes(int B, int C, int H, int W, int K);
 int launch_select(const float* heat, const int64_t st[4], int B, int C, int H, int W, int nms, int apply_sigmoid,
                   int K, void* ws, size_t ws_bytes, float* score, int32_t* index, const DecodeParams* rec,
                   hipStream_t s);
+// tv_decode's path (sigmoid + 3x3 NMS + exact top-K + records): peak_scan + peak_select
+// (decode.hip), workspace decode_workspace_bytes() (no initial contents needed).
+size_t decode_workspace_bytes(int B, int C, int H, int W, int K);
+int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, int W, int K, void* ws,
+                  size_t ws_bytes, const DecodeParams& rec, hipStream_t s);
 // heatmap_detect()'s (index[B,K,2], label[B,K]) as int64 from flat top-K indices.
 int launch_index_split(const int32_t* flat, int B, int K, int H, int W, int64_t* index, int64_t* label,
                        hipStream_t s);

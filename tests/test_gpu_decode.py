@@ -192,3 +192,46 @@ def test_fused_decode_matches_oracle_large_batch():
     np.testing.assert_array_equal(rec[..., 5], size.numpy()[bi, iy, ix, 1])
     y = ((4.0 * iy + offset.numpy()[bi, iy, ix, 0].astype(np.float64)) / 480).astype(np.float32)
     np.testing.assert_array_equal(rec[..., 2], y)
+
+
+def test_decode_fallback_and_workspace_reuse():
+    """Images with fewer than K positive peaks (sigmoid saturated to 0: the exact streaming path)
+    next to ordinary ones, decoded three times through one DeviceDecoder with the images rotated
+    (the per-tile key segments of one call must not leak into the next)."""
+    from tauv_vision_amd.decode import DeviceDecoder
+    B, C, H, W, K = 3, 2, 20, 30, 50
+    g = torch.Generator().manual_seed(5)
+    logits = torch.full((B, C, H, W), -200.0)              # image 0: every score 0
+    pos = torch.randperm(C * H * W, generator=g)[:10]      # image 1: 10 positive peaks < K
+    logits[1].view(-1)[pos] = torch.rand(10, generator=g) * 4.0
+    logits[2] = torch.randn((C, H, W), generator=g) * 2.0  # image 2: the fast path
+    size = torch.randn((B, H, W, 2), generator=g)
+    offset = torch.rand((B, H, W, 2), generator=g)
+    dec = DeviceDecoder(B, C, H, W, K, torch.device("cuda"))
+    for order in ([0, 1, 2], [2, 0, 1], [1, 2, 0]):
+        lg = logits[order]
+        rec, cnt = dec(lg.cuda(), size.cuda(), offset.cuda(), None, 0, 4, 80, 120, 0.0)
+        rec = rec.cpu().numpy()
+        nms = oracle.heatmap_nms(torch.sigmoid(lg), 3).reshape(B, -1).numpy()
+        ref_s, ref_i = _tie_rule_topk(nms, K)
+        np.testing.assert_array_equal(rec[..., 7].astype(np.int64), ref_i)
+        np.testing.assert_allclose(rec[..., 1], ref_s, rtol=0, atol=1e-6)
+        assert (cnt.cpu().numpy() == K).all()
+
+
+def test_decode_nhwc_aligned_heads_match_nchw():
+    """The engine's head tensor layout (NHWC, 4 heat channels first, pixel stride a multiple of
+    4 floats: the float4 fill path of peak_scan) decodes exactly as the plain NCHW tensors."""
+    from tauv_vision_amd.decode import DeviceDecoder
+    g = torch.Generator().manual_seed(11)
+    B, C, H, W, K = 5, 4, 60, 80, 100
+    logits = torch.randn((B, C, H, W), generator=g) * 2.0
+    size = torch.randn((B, H, W, 2), generator=g)
+    offset = torch.rand((B, H, W, 2), generator=g)
+    nhwc = torch.cat([logits.permute(0, 2, 3, 1), size, offset], dim=3).contiguous().cuda()  # 8 channels
+    dec = DeviceDecoder(B, C, H, W, K, torch.device("cuda"))
+    r1, c1 = dec(nhwc[..., 0:4].permute(0, 3, 1, 2), nhwc[..., 4:6], nhwc[..., 6:8], None, 0, 4, 240, 320, 0.2)
+    r1, c1 = r1.cpu().numpy().copy(), c1.cpu().numpy().copy()
+    r2, c2 = dec(logits.cuda(), size.cuda(), offset.cuda(), None, 0, 4, 240, 320, 0.2)
+    np.testing.assert_array_equal(r1, r2.cpu().numpy())
+    np.testing.assert_array_equal(c1, c2.cpu().numpy())

@@ -545,13 +545,10 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv) {
 // one float4 per pixel) or column-fastest (0: NCHW).
 template <int CHAN_FAST>
 __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restrict__ heat, int64_t s0, int s1, int s2,
-                                                           int s3, int C, int H, int W, int K, const TileGeom g,
+                                                           int s3, int C, int H, int W, const TileGeom g,
                                                            const ScanWs w) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ uint32_t wsum[kScanThreads / 64 + 1];
-  __shared__ uint32_t fhist[256];
-  __shared__ int red_n[kScanThreads / 64];
-  __shared__ int keep_digit;
   const int b = blockIdx.y;
   int t = blockIdx.x;
   const int tx = t % g.ntw; t /= g.ntw;
@@ -560,9 +557,6 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
   const int c0 = tc * g.cg, y0 = ty * g.th, x0 = tx * g.tw;
   const int nc = min(g.cg, C - c0), nh = min(g.th, H - y0), nw = min(g.tw, W - x0);
   const int LH = nh + 2, LW = nw + 2;
-  const int LP = ((LW + 3) & ~3) + 4;  // LDS row pitch (floats): 16-byte rows, room for the last strip's window
-  fhist[threadIdx.x] = 0;
-  static_assert(kScanThreads == 256, "one filter-histogram bin per thread");
   const float* base = heat + b * s0 + c0 * s1;
 
   // tile + halo -> LDS [cc][yy][xx], sigmoid once per element, outside the image -inf
@@ -586,14 +580,14 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
         const bool in = pp < np && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
         inb[j] = in;
         v[j] = in ? *reinterpret_cast<const float4*>(base + y * s2 + x * s3) : make_float4(0.f, 0.f, 0.f, 0.f);
-        pix[j] = pp < np ? yy * LP + xx : -1;
+        pix[j] = pp < np ? pp : -1;
       }
 #pragma unroll
       for (int j = 0; j < kFillBatch; ++j) {
         if (pix[j] < 0) continue;
         const float e[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) tile[cc * LH * LP + pix[j]] = inb[j] ? sigmoidf_ref(e[cc]) : -INFINITY;
+        for (int cc = 0; cc < 4; ++cc) tile[cc * np + pix[j]] = inb[j] ? sigmoidf_ref(e[cc]) : -INFINITY;
       }
     }
   } else
@@ -620,7 +614,7 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
       const bool in = e < nl && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
       inb[j] = in;
       v[j] = in ? base[cc * s1 + y * s2 + x * s3] : 0.f;
-      dst[j] = e < nl ? (cc * LH + yy) * LP + xx : -1;
+      dst[j] = e < nl ? (cc * LH + yy) * LW + xx : -1;
     }
 #pragma unroll
     for (int j = 0; j < kFillBatch; ++j)
@@ -645,17 +639,12 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
     const int cc = fdiv(p, nh, inv_nh);
     const int yy = p - cc * nh;
     const int xb = 4 * xs;
-    // window rows yy .. yy + 2, columns xb .. xb + 5 (16 + 8 bytes per row; columns past LW only
-    // reach the masked elements of a partial strip)
-    const float* r0 = tile + (cc * LH + yy) * LP + xb;
+    const float* r0 = tile + (cc * LH + yy) * LW + xb;  // window rows yy .. yy + 2, columns xb .. xb + 5
     float win[3][6];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const float4 a4 = *reinterpret_cast<const float4*>(r0 + r * LP);
-      const float2 a2 = *reinterpret_cast<const float2*>(r0 + r * LP + 4);
-      win[r][0] = a4.x; win[r][1] = a4.y; win[r][2] = a4.z; win[r][3] = a4.w;
-      win[r][4] = a2.x; win[r][5] = a2.y;
-    }
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) win[r][c] = (xb + c < LW) ? r0[r * LW + c] : -INFINITY;
     const uint32_t flat0 = (uint32_t)(((c0 + cc) * H + y0 + yy) * W + x0 + xb);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -672,9 +661,8 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
       mine += keep ? 1u : 0u;
     }
   }
+  // compact into the tile's segment: wave prefix + wave offsets
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // compact the tile's positive keys into LDS (over the tile's sigmoid values: the NMS is done)
-  uint64_t* list = reinterpret_cast<uint64_t*>(tile);
   uint32_t incl = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -682,98 +670,20 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
     if (lane >= o) incl += u;
   }
   if (lane == 63) wsum[wave] = incl;
-  __syncthreads();  // every wave is past its window reads: the tile LDS may be overwritten
-  uint32_t off = 0, nk = 0;
-#pragma unroll
-  for (int i = 0; i < kScanThreads / 64; ++i) {
-    off += i < wave ? wsum[i] : 0u;
-    nk += wsum[i];
-  }
-  {
-    uint64_t* d = list + off + (incl - mine);
-#pragma unroll
-    for (int j = 0; j < kScanPer; ++j)
-      if (k[j]) *d++ = k[j];
-  }
   __syncthreads();
-  // per-tile pre-filter: every key of the image's top K is among its tile's top K, so when the
-  // tile has more than K keep only those whose 8-bit score digit (just below the score bits all
-  // the tile's keys share) reaches the digit of the tile's K-th largest — K plus at most one
-  // digit's worth instead of every peak. Ties in score share a digit, so they stay together.
-  uint32_t kd = 0;
-  int sh = 0;
-  if ((int)nk > K) {  // uniform
-    uint32_t lo = ~0u, hi = 0;
-    for (uint32_t i = threadIdx.x; i < nk; i += kScanThreads) {
-      const uint32_t sc = (uint32_t)(list[i] >> 32);
-      lo = sc < lo ? sc : lo;
-      hi = sc > hi ? sc : hi;
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      const uint32_t l = (uint32_t)__shfl_xor((int)lo, o), h = (uint32_t)__shfl_xor((int)hi, o);
-      lo = l < lo ? l : lo;
-      hi = h > hi ? h : hi;
-    }
-    if (lane == 0) { red_n[wave] = (int)lo; wsum[wave] = hi; }
-    __syncthreads();
-    lo = ~0u; hi = 0;
-#pragma unroll
-    for (int i = 0; i < kScanThreads / 64; ++i) {
-      lo = (uint32_t)red_n[i] < lo ? (uint32_t)red_n[i] : lo;
-      hi = wsum[i] > hi ? wsum[i] : hi;
-    }
-    const uint32_t diff = lo ^ hi;
-    if (diff) {
-      const int msb = 31 - __builtin_clz(diff);
-      sh = msb > 7 ? msb - 7 : 0;
-      for (uint32_t i0 = 0; i0 < nk; i0 += kScanThreads) {
-        const uint32_t i = i0 + threadIdx.x;
-        hist_add(fhist, i < nk ? (uint32_t)(list[i] >> (32 + sh)) & 255u : 0u, i < nk);
-      }
-      __syncthreads();
-      // thread t owns digit 255 - t; running count from the top
-      const int c = (int)fhist[255 - threadIdx.x];
-      int inc2 = c;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(inc2, o);
-        if (lane >= o) inc2 += u;
-      }
-      __syncthreads();  // the min / max slots are read: reuse red_n for the wave totals
-      if (lane == 63) red_n[wave] = inc2;
-      __syncthreads();
-      int before = inc2 - c;
-#pragma unroll
-      for (int i = 0; i < kScanThreads / 64; ++i) before += i < wave ? red_n[i] : 0;
-      if (before < K && K <= before + c) keep_digit = 255 - (int)threadIdx.x;
-      __syncthreads();
-      kd = (uint32_t)keep_digit;
-    }
-  }
-  // the kept keys -> the tile's segment (ballot positions), and the count
+  uint32_t off = 0;
+  for (int i = 0; i < wave; ++i) off += wsum[i];
   const size_t seg = (size_t)b * w.tiles + blockIdx.x;
-  uint64_t* dst = w.keys + seg * kScanElems;
-  uint32_t pos = 0;
-  const uint64_t lt = (1ull << lane) - 1;
-  for (uint32_t i0 = 0; i0 < nk; i0 += kScanThreads) {
-    const uint32_t i = i0 + threadIdx.x;
-    const uint64_t key = i < nk ? list[i] : 0;
-    const bool keep = i < nk && ((uint32_t)(key >> (32 + sh)) & 255u) >= kd;
-    const uint64_t bal = __ballot(keep);
-    if (lane == 0) wsum[wave] = (uint32_t)__popcll(bal);
-    __syncthreads();
-    uint32_t wo = 0, tot = 0;
+  uint64_t* dst = w.keys + seg * kScanElems + off + (incl - mine);
 #pragma unroll
-    for (int w2 = 0; w2 < kScanThreads / 64; ++w2) {
-      wo += w2 < wave ? wsum[w2] : 0u;
-      tot += wsum[w2];
-    }
-    if (keep) dst[pos + wo + (uint32_t)__popcll(bal & lt)] = key;
-    pos += tot;
-    __syncthreads();
+  for (int j = 0; j < kScanPer; ++j)
+    if (k[j]) *dst++ = k[j];
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int i = 0; i < kScanThreads / 64; ++i) tot += wsum[i];
+    w.cnt[seg] = tot;
   }
-  if (threadIdx.x == 0) w.cnt[seg] = pos;
 }
 
 // key of flat element e of image b, recomputed from the heatmap exactly as peak_scan / tile_select
@@ -827,6 +737,8 @@ __device__ void topdown_pick(const uint32_t (&c)[4], int D, int need, SelectShar
 
 constexpr int kSelThreads = 1024;
 
+__device__ unsigned g_st[64][8];
+#define ST(i) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_st[blockIdx.x][i] = (unsigned)wall_clock64(); } while (0)
 __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restrict__ heat, int64_t s0, int64_t s1,
                                                              int64_t s2, int64_t s3, int H, int W, int K,
                                                              const ScanWs w, const MergeOut mo, const DecodeParams p) {
@@ -841,6 +753,7 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
   uint16_t* segmap = reinterpret_cast<uint16_t*>(pool);
   static_assert(sizeof(pool) >= 16384 * 2 && kMaxScanTiles <= 65536, "segment map");
   const int b = blockIdx.x, tid = threadIdx.x;
+  ST(0);
   const int lane = tid & 63, wave = tid >> 6;
   constexpr int NWAVE = kSelThreads / 64;
   constexpr int KPT = 16;  // keys per thread when the image's positive keys fit in registers
@@ -875,6 +788,7 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
     __syncthreads();
   }
   const int n = sh.nreal;
+  ST(1);
   // the keys in registers when they fit (key i = tid + j * NT), through a key -> segment map
   const bool cached = n <= KPT * kSelThreads;
   uint64_t rk[KPT];
@@ -893,6 +807,7 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
     }
     __syncthreads();  // the map is dead: lh / cand / top reuse its LDS
   }
+  ST(2);
   for (int i = tid; i < kHistBins; i += kSelThreads) lh[i] = 0;
   __syncthreads();
   // every positive key of the image (wave-uniform calls): registers, or the segments in global
@@ -915,6 +830,7 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
     }
   };
 
+  ST(3);
   if (n >= K) {
     const int cap = K > kRankCap ? K : kRankCap;
     // level 0: the 12 bits just below the bits every key shares (block min / max), so a map
@@ -940,6 +856,7 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
 #pragma unroll
     for (int i = 0; i < 4; ++i) c4[i] = lh[kHistBins - 1 - 4 * tid - i];
     topdown_pick<kSelThreads>(c4, kHistBins, K, sh);
+  ST(4);
     uint64_t prefix = (common << kHistBits) | (uint64_t)sh.sel_digit;
     int above = sh.sel_above, bc = sh.sel_count;
     __syncthreads();
@@ -966,6 +883,7 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
       shift = ns;
       __syncthreads();
     }
+  ST(5);
     // candidates: every key whose top bits are >= the threshold digit path (above + bc of them)
     if (cached) {
       // wave counts -> wave offsets (one barrier), then ballot positions: no returning atomics
@@ -995,6 +913,7 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
     }
     __syncthreads();
     const int m = ncand;
+  ST(6);
     if (m <= kSelThreads / 4) {
       // four threads per candidate (adjacent lanes), each counting a quarter of the larger keys
       const int ci = tid >> 2, part = tid & 3;
@@ -1046,7 +965,10 @@ __global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restri
     __syncthreads();
     bitonic_desc<kSelThreads>(top, P);
   }
+  ST(7);
   write_outputs<kSelThreads>(top, K, b, mo, p, cnt_thr);
+  __syncthreads();
+  if (tid < 8 && b < 64) reinterpret_cast<unsigned*>(p.records)[((size_t)b * K + (K - 1)) * 10 + tid] = g_st[b][tid];
 }
 
 // ---- host side --------------------------------------------------------------------------
@@ -1160,9 +1082,7 @@ int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, i
   const TileGeom g = scan_geom(C, H, W, st[1] < st[3] ? 1 : 0);
   const int tiles = g.ncg * g.nth * g.ntw;
   if (tiles > kMaxScanTiles || B > 65535) { set_error("decode: heatmap too large (tiles per image)"); return 1; }
-  // the tile (+ halo) in fp32, later reused for the tile's compacted keys
-  const size_t lds = std::max((size_t)g.cg * (g.th + 2) * ((((g.tw + 2) + 3) & ~3) + 4) * sizeof(float),
-                              (size_t)kScanElems * sizeof(uint64_t));
+  const size_t lds = (size_t)g.cg * (g.th + 2) * (g.tw + 2) * sizeof(float);
   ScanWs w;
   w.cnt = (uint32_t*)ws;
   w.keys = (uint64_t*)((char*)ws + ((size_t)B * tiles * 4 + 255) / 256 * 256);
@@ -1178,13 +1098,13 @@ int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, i
                     st[0] % 4 == 0 && ((uintptr_t)heat & 15) == 0;
   if (vec4)
     hipLaunchKernelGGL(peak_scan<2>, dim3(tiles, B), dim3(kScanThreads), lds, s, heat, st[0], (int)st[1], (int)st[2],
-                       (int)st[3], C, H, W, K, g, w);
+                       (int)st[3], C, H, W, g, w);
   else if (g.chan_fast)
     hipLaunchKernelGGL(peak_scan<1>, dim3(tiles, B), dim3(kScanThreads), lds, s, heat, st[0], (int)st[1], (int)st[2],
-                       (int)st[3], C, H, W, K, g, w);
+                       (int)st[3], C, H, W, g, w);
   else
     hipLaunchKernelGGL(peak_scan<0>, dim3(tiles, B), dim3(kScanThreads), lds, s, heat, st[0], (int)st[1], (int)st[2],
-                       (int)st[3], C, H, W, K, g, w);
+                       (int)st[3], C, H, W, g, w);
   TV_HIP(hipGetLastError());
   MergeOut mo{nullptr, nullptr, 1};
   hipLaunchKernelGGL(peak_select, dim3(B), dim3(kSelThreads), 0, s, heat, st[0], st[1], st[2], st[3], H, W, K, w, mo,

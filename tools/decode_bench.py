@@ -1,4 +1,4 @@
-"""Decode timing probe: DeviceDecoder (tile_select + merge_select) on a real R18 head tensor
+"""Decode timing probe: DeviceDecoder (peak_scan + peak_select) on a real R18 head tensor
 and on random logits, B in {1, 64}, K in {1, 10, 100}; HIP-event time per call (min of 20)."""
 import os
 import sys
@@ -34,9 +34,10 @@ pipe = bench.Pipeline(model, oc, mc, 64, 100, 0.3, dev)
 pipe.eng.forward_u8(frames, pipe.out)
 p = pipe.pred
 only = "--only" in sys.argv  # the bench configuration alone (B=64, K=100, R18 heads)
-for name, heat in (("r18", p.heatmap), ("rand", (torch.rand_like(p.heatmap) * 9 - 8)))[:1 if only else 2]:
-    for B in ((64,) if only else (64, 1)):
-        for K in ((100,) if only else (100, 10, 1)):
+only1 = "--only1" in sys.argv  # the B=1 latency configuration alone
+for name, heat in (("r18", p.heatmap), ("rand", (torch.rand_like(p.heatmap) * 9 - 8)))[:1 if only or only1 else 2]:
+    for B in ((64,) if only else (1,) if only1 else (64, 1)):
+        for K in ((100,) if only or only1 else (100, 10, 1)):
             d = DeviceDecoder(B, 4, 120, 160, K, dev)
             us = t_call(lambda: d(heat[:B], p.size[:B], p.offset[:B], None, 0, 4, 480, 640, 0.3))
             print(f"{name:5s} B={B:3d} K={K:3d}: {us:8.1f} us", flush=True)

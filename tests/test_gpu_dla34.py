@@ -110,3 +110,27 @@ def test_dla34_u8_frames_and_batch_independence():
     scale = max(1.0, float(b.abs().max()))
     assert float((a - b).abs().max()) <= 2e-2 * scale
     assert float((b[1:2] - c).abs().max()) <= 1e-3 * scale
+
+
+def test_dla34_batch64_slices_consistent():
+    """B=64 at the production 480x640 size (two concurrent 32-frame slices on side streams, the
+    bench configuration): frames that repeat across the batch give identical outputs wherever
+    they sit (slice boundaries, stream placement), and match a B=1 forward of the same frame."""
+    name = "b1_480x640_kp"
+    model, oc, mc, case = build(name, "fp16")
+    g = torch.Generator().manual_seed(9)
+    base = torch.randint(0, 256, (4, case["in_h"], case["in_w"], 3), generator=g, dtype=torch.uint8)
+    frames = base.repeat(16, 1, 1, 1).cuda()  # frame i == base[i % 4]
+    with torch.no_grad():
+        big = model.forward_frames(frames)
+        one = model.forward_frames(frames[:1])
+    for f in ("heatmap", "size", "offset", "keypoint_heatmap"):
+        t = getattr(big, f)
+        if t is None:
+            continue
+        t = t.float().cpu()
+        for i in range(4, 64):
+            assert torch.equal(t[i], t[i % 4]), (f, i)
+        o = getattr(one, f).float().cpu()
+        scale = max(1.0, float(o.abs().max()))
+        assert float((t[0] - o[0]).abs().max()) <= 1e-3 * scale, f

@@ -33,8 +33,7 @@ size_t conv3x3_weight_bytes(int ntiles, int res, int ncb) {
 }
 
 int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, void* out, hipStream_t s) {
-  if ((Kpad * esz) % 16 || Kpad < (9 + res) * 32 * ncb || (ni != 4 && ni != 2) || (ncb != 2 && ncb != 4 && ncb != 8) ||
-      (res && ncb != 4)) {
+  if ((Kpad * esz) % 16 || Kpad < (9 + res) * 32 * ncb || (ni != 4 && ni != 2) || (ncb != 2 && ncb != 4 && ncb != 8)) {
     set_error("conv3x3_repack: bad Kpad / ni / channel blocks");
     return 1;
   }
@@ -52,12 +51,12 @@ int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dty
     return 1;
   }
   const int ncb = p.seg[0].C / CBK;
-  if ((ncb != 2 && ncb != 4 && ncb != 8) || (ncb != 4 && res)) {
-    set_error("conv3x3: inputs of 64, 128 or 256 channels (residual k-steps: 128)");
+  if (ncb != 2 && ncb != 4 && ncb != 8) {
+    set_error("conv3x3: inputs of 64, 128 or 256 channels");
     return 1;
   }
-  if (ncb == 2) return launch_ncb2(p, dp, out, dtype, tw, grid, s, epi, ni);
-  if (ncb == 8) return launch_ncb8(p, dp, out, dtype, tw, grid, s, epi, ni);
+  if (ncb == 2) return launch_ncb2(p, dp, out, dtype, tw, grid, s, epi, res, ni);
+  if (ncb == 8) return launch_ncb8(p, dp, out, dtype, tw, grid, s, epi, res, ni);
   return launch_ncb4(p, dp, out, dtype, tw, grid, s, epi, res, ni);
 }
 

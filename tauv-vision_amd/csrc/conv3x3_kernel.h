@@ -142,7 +142,6 @@ template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI, 
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
   static_assert(NI == 4 || (NI == 2 && EPI == 0), "half tiles: plain epilogue only");
-  static_assert(!RES || NCB == 4, "residual k-steps: 128-channel inputs only");
   constexpr int SPTK = spt<RES, NCB>();  // k-steps per tile
   constexpr int BNK = 32 * NI;      // output channels per tile
   constexpr int WSL = BNK * 64;     // weight bytes per k-step (an LDS ring slot holds up to WSLOT)
@@ -263,8 +262,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
                         cb * CBK * (int)sizeof(T), 0, 0);
   };
 
-  // ---- RES: the ResidualBlock's 1x1 conv_residual (dla.py:32-37) as a 10th k-step per
-  // channel block. Its input x (second segment, stride rstr) for the tile's 512 output pixels
+  // ---- RES: the ResidualBlock's 1x1 conv_residual (dla.py:32-37), or DLA-34 BasicBlock's identity
+  // residual (centerpoint_dla.py:30-59, an identity 1x1), as a 10th k-step per channel block. Its input x (second segment, stride rstr) for the tile's 512 output pixels
   // moves into one 32 KiB LDS buffer per channel block: chunk L = piece*64 + lane holds pixel
   // q = L/4, source chunk (L % 4) ^ ((q >> 2) & 3) (conflict-free fragment reads). One buffer
   // resource per frame keeps offsets below 2^31.
@@ -289,7 +288,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     rs.w = 0x00020000;
     const int q = (int)(rgeo[i] >> 2), c = (int)(rgeo[i] & 3);
     const int y = y0 + q / TW, x = x0 + q % TW;
-    const bool ok = y < H && x < W;
+    const bool ok = y < H && x < W && fr < nframes;  // a phantom unit's frame is past the tensor: OOB zeros
     const unsigned off = ok ? ((unsigned)(y * sr.stride) * (unsigned)sr.W + (unsigned)(x * sr.stride)) * rpix_bytes +
                                   (unsigned)c * 16u
                             : 0x80000000u;
@@ -661,11 +660,30 @@ inline int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int gr
 using Launch = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
 // per input-channel-count instance tables (conv3x3_n2/n4/n8.hip)
 int launch_ncb2(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,
-                int epi, int ni);
+                int epi, int res, int ni);
 int launch_ncb4(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,
                 int epi, int res, int ni);
 int launch_ncb8(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,
-                int epi, int ni);
+                int epi, int res, int ni);
+// the residual (RES) instances of a channel-block count: ReLU, plain stores, [bf16][tw == 32][ni == 4]
+template <int NCB>
+int launch_res(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,
+               int epi, int ni) {
+  if (p.act != 1 || epi != 0 || p.nseg != 2) {
+    set_error("conv3x3: residual k-steps need ReLU, plain stores and two segments");
+    return 1;
+  }
+  static const Launch r[2][2][2] = {
+      {{launch_t<_Float16, 16, 1, 0, 1, 2, NCB>, launch_t<_Float16, 16, 1, 0, 1, 4, NCB>},
+       {launch_t<_Float16, 32, 1, 0, 1, 2, NCB>, launch_t<_Float16, 32, 1, 0, 1, 4, NCB>}},
+      {{launch_t<__bf16, 16, 1, 0, 1, 2, NCB>, launch_t<__bf16, 16, 1, 0, 1, 4, NCB>},
+       {launch_t<__bf16, 32, 1, 0, 1, 2, NCB>, launch_t<__bf16, 32, 1, 0, 1, 4, NCB>}}};
+  if (dtype != F16 && dtype != BF16) {
+    set_error("conv3x3: fp16/bf16 only");
+    return 1;
+  }
+  return r[dtype == BF16][tw == 32][ni == 4](p, dp, out, grid, s);
+}
 
 }  // namespace c3
 }  // namespace tv

@@ -5,7 +5,8 @@ namespace tv {
 namespace c3 {
 
 int launch_ncb2(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s, int epi,
-                int ni) {
+                int res, int ni) {
+  if (res) return launch_res<2>(p, dp, out, dtype, tw, grid, s, epi, ni);  // DLA-34 BasicBlock identity residual
   // 64-channel inputs (DLA-34 level 2 and its up-path, the stacked DLA-34 heads)
     if (epi == 1) {
       if (p.act < 1 || p.ntiles > 16) {

@@ -6,20 +6,7 @@ namespace c3 {
 
 int launch_ncb4(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s, int epi,
                 int res, int ni) {
-  if (res) {  // ResidualBlock conv2 + conv_residual: ReLU, plain stores
-    if (p.act != 1 || epi != 0 || p.nseg != 2 || p.ntiles != 1) {
-      set_error("conv3x3: residual k-steps need ReLU, one channel tile and two segments");
-      return 1;
-    }
-    static const Launch r16[2][2] = {{launch_t<_Float16, 16, 1, 0, 1, 2>, launch_t<_Float16, 16, 1, 0, 1, 4>},
-                                {launch_t<_Float16, 32, 1, 0, 1, 2>, launch_t<_Float16, 32, 1, 0, 1, 4>}};
-    static const Launch rb16[2][2] = {{launch_t<__bf16, 16, 1, 0, 1, 2>, launch_t<__bf16, 16, 1, 0, 1, 4>},
-                                 {launch_t<__bf16, 32, 1, 0, 1, 2>, launch_t<__bf16, 32, 1, 0, 1, 4>}};
-    if (dtype == F16) return r16[tw == 32][ni == 4](p, dp, out, grid, s);
-    if (dtype == BF16) return rb16[tw == 32][ni == 4](p, dp, out, grid, s);
-    set_error("conv3x3: fp16/bf16 only");
-    return 1;
-  }
+  if (res) return launch_res<4>(p, dp, out, dtype, tw, grid, s, epi, ni);  // ResidualBlock conv2 + conv_residual
   if (epi == 1) {  // fused 1x1 heads: the stacked heads' LeakyReLU only
     if (p.act != 2 || p.ntiles > 16) {
       set_error("conv3x3: fused heads need LeakyReLU and <= 16 channel tiles");

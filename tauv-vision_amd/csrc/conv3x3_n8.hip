@@ -5,7 +5,8 @@ namespace tv {
 namespace c3 {
 
 int launch_ncb8(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s, int epi,
-                int ni) {
+                int res, int ni) {
+  if (res) return launch_res<8>(p, dp, out, dtype, tw, grid, s, epi, ni);  // DLA-34 BasicBlock identity residual
   // 256-channel inputs (protonet, DLA-34 level 4)
     if (epi == 1) {
       if (p.act != 2 || p.ntiles > 16) {

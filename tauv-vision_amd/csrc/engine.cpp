@@ -523,8 +523,9 @@ int Engine::make_workspace(int B, Workspace* ws) {
     // channels, fp16/bf16, 16-byte aligned channel slices, byte offsets within 2^31
     // A second segment is accepted when it is ResidualBlock's 1x1 conv_residual (128 channels,
     // stride 1 or 2, ReLU after the sum): one extra k-step per channel block (RES).
+    // (or DLA-34 BasicBlock's identity residual: 64 / 128 / 256 channels, an identity 1x1)
     const bool res2 = op.segs.size() == 2 && op.segs[1].kh == 1 && op.segs[1].kw == 1 && op.segs[1].pad == 0 &&
-                      p.seg[1].C == 128 && p.seg[1].ldc % 8 == 0 && p.N == 128 && p.ntiles == 1 && op.act == 1 &&
+                      p.seg[1].C == p.seg[0].C && p.seg[1].ldc % 8 == 0 && p.N == p.seg[1].C && op.act == 1 &&
                       (size_t)p.seg[1].H * p.seg[1].W * p.seg[1].ldc * esz < (1ull << 31) &&
                       p.seg[1].H >= (p.Ho - 1) * p.seg[1].stride + 1 && p.seg[1].W >= (p.Wo - 1) * p.seg[1].stride + 1;
     if (conv3_mode && dtype != F32 && op.kind == OP_CONV && (op.segs.size() == 1 || res2) && op.out >= 0 &&
@@ -534,7 +535,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
       const size_t src_bytes = (size_t)B * cs.H * cs.W * cs.ldc * esz;
       if (sg.kh == 3 && sg.kw == 3 && sg.stride == 1 && sg.pad == 1 && pw == 1 && !sg.row_expand &&
-          (cs.C == 128 || ((cs.C == 256 || cs.C == 64) && !res2)) &&
+          (cs.C == 128 || cs.C == 256 || cs.C == 64) &&
           cs.ldc % 8 == 0 && p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && src_bytes < (1ull << 31) &&
           p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix &&
           (size_t)cs.H * cs.W * p.out_ldc * esz < (1ull << 31)) {
@@ -547,7 +548,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
         const long t4 = (long)mt * p.ntiles;
         const long r4 = (t4 + cu_count - 1) / cu_count, r2 = (2 * t4 + cu_count - 1) / cu_count;
         int ni = c3_ni_force ? c3_ni_force : (c3_half_cost > 0 && c3_half_cost * r2 < 100 * r4) ? 2 : 4;
-        if (p.N <= 64 && !res) ni = 2;  // one 64-channel half tile holds every output channel
+        if (p.N <= 64) ni = 2;  // one 64-channel half tile holds every output channel
         if (op.act >= 1 && !res && op.out >= 0 && i + 1 < plan.ops.size() && !plan.ops[i + 1].diag_in_off.empty())
           ni = 4;  // the stacked heads (fused 1x1 epilogue) keep 128-channel tiles
         const long total = (ni == 2 && p.N <= 64) ? t4 : t4 * (4 / ni);

@@ -48,10 +48,15 @@ typedef enum tv_dtype { TV_F32 = 0, TV_F16 = 1, TV_BF16 = 2 } tv_dtype;
  * are ignored); TV_ARCH_PROTONET = the YOLACT protonet Masknet (masknet.py:8-55): channels[0] =
  * feature_depth, head_channels[0] = n_prototype_masks, (in_h, in_w) = the fpn[0] feature size;
  * tv_engine_forward takes fpn[0] as fp32 NCHW [B, feature_depth, in_h, in_w] and writes the
- * prototypes as fp32 NHWC [B, 4 in_h, 4 in_w, out_cpad]. */
+ * prototypes as fp32 NHWC [B, 4 in_h, 4 in_w, out_cpad]; TV_ARCH_CENTERNET_BACKBONE = the
+ * DLABackbone alone (dla.py:393-416, DLABackbone.forward): the parameters are the "backbone.*"
+ * keys of TV_ARCH_CENTERNET, n_heads / head_channels are ignored, and the output is the
+ * IDAUpReverse feature map as fp32 NHWC [B, in_h / 2^downsamples, in_w / 2^downsamples,
+ * channels[0]]. */
 #define TV_ARCH_CENTERNET 0
 #define TV_ARCH_DLA34 1
 #define TV_ARCH_PROTONET 2
+#define TV_ARCH_CENTERNET_BACKBONE 3
 typedef struct tv_model_desc {
   int32_t n_levels;          /* len(backbone_heights) */
   int32_t heights[8];        /* backbone_heights */

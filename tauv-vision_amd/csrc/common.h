@@ -89,12 +89,18 @@ struct ConvParams {
   const float* head_b;  // [ntiles][32] 1x1 bias on the first tile of each head, zeros elsewhere
   int head_ldc;
   int head_row0[16], head_nrows[16];
+  int flags;            // halo kernels: bit 0 = static s_setprio 1 for the younger half (waves 4-7)
 };
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
 int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
                      hipStream_t s);
 constexpr int kPipeTileM = 256;
+// Split-K variant for the small levels (conv_lat.hip): 64-pixel x 128-channel tiles, the k-step
+// descriptors split over two 4-wave K groups; ConvParams.mtiles / ntiles from conv_lat_tiles();
+// mode-0 k-steps only (every segment's channel count a multiple of 64 / 128 bytes)
+int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles);
+int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s);
 
 // Persistent halo-tile 3x3 / stride 1 / pad 1 kernel (conv3x3.hip), fp16/bf16, 128- or 256-channel
 // input (seg[0].C): 512-pixel

@@ -192,6 +192,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int ntl = first < end ? UP * ((end - first + stride - 1) / stride) : 0;
   if (ntl == 0) return;
   const int S_tot = ntl * SPTK;
+  // the second-dispatched half of the workgroup loses VALU / issue arbitration to the older
+  // half on every segment; one static priority raise (no per-segment flips) evens it out
+  if (p.flags & 1)
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   // bias of every output channel into LDS (read in the epilogues)
   float* lbias = reinterpret_cast<float*>(smem + OFF_B);

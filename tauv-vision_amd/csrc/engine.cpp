@@ -296,6 +296,9 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_C3_TW")) c3_tw_force = std::atoi(env) == 16 ? 16 : std::atoi(env) == 32 ? 32 : 0;
   if (const char* env = std::getenv("TV_CUS")) cu_count = std::max(8, std::min(cu_count, std::atoi(env)));
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_LAT")) lat_mode = std::atoi(env);
+  if (const char* env = std::getenv("TV_LAT_UNITS")) lat_units = std::atoi(env);
+  if (const char* env = std::getenv("TV_PRIO")) prio_young = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
@@ -471,6 +474,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   const int BK = 128 / esz;
   std::vector<KStep> all_ks;
   std::vector<size_t> ks_off(plan.ops.size(), 0);
+  std::vector<std::vector<KStep>> op_ks(plan.ops.size());  // per op: its k-steps when all are mode 0
   ws->use_pipe.assign(plan.ops.size(), 0);
   ws->kname.assign(plan.ops.size(), std::string());
   ws->c3_tw.assign(plan.ops.size(), 0);
@@ -509,6 +513,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
         ks.push_back(d);
       }
     }
+    if (ok && std::all_of(ks.begin(), ks.end(), [](const KStep& d) { return d.mode == 0; })) op_ks[i] = ks;
     const int mt = (p.M + kPipeTileM - 1) / kPipeTileM;
     const bool big = (long)mt * p.ntiles >= 256;
     ws->use_pipe[i] = ok && (pipe_mode == 1 || (pipe_mode < 0 && big));
@@ -519,6 +524,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.mtiles = mt;
     }
     p.zero = zero_page;
+    p.flags = prio_young ? 1 : 0;
     // persistent halo-tile 3x3 kernel (conv3x3.hip): 3x3 / stride 1 / pad 1, one input of 128
     // channels, fp16/bf16, 16-byte aligned channel slices, byte offsets within 2^31
     // A second segment is accepted when it is ResidualBlock's 1x1 conv_residual (128 channels,
@@ -703,11 +709,48 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->convt[i] = 1;
     ws->use_pipe[i] = 0;
   }
+  // layers the chosen kernel spreads over fewer work units than the threshold (the deep pyramid
+  // levels: a few 512-pixel tiles on 256 CUs) -> conv_lat.hip (small tiles, K split over waves)
+  ws->lat.assign(plan.ops.size(), 0);
+  const int lat_min = lat_units >= 0 ? lat_units : cu_count;
+  for (size_t i = 0; lat_mode && dtype != F32 && i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    ConvParams& p = ws->params[i];
+    if (op.kind != OP_CONV || op.up_s || op.out < 0 || op.add >= 0 || (int)i == stem_op || op_ks[i].empty() ||
+        ws->small[i] || ws->dcn[i].x || ws->dcn_skip[i] || ws->head_fused[i] || ws->head_skip[i] || p.N % 8 ||
+        p.out_ldc % 8 || p.out_coff % 8)
+      continue;
+    long units;
+    if (ws->c3_tw[i]) units = (long)p.mtiles * p.ntiles * (ws->c3_ni[i] == 2 && p.N > 64 ? 2 : 1);
+    else if (ws->s2_grid[i]) units = p.mtiles;
+    else if (ws->use_pipe[i]) units = (long)p.mtiles * p.ntiles;
+    else units = 0;  // conv_igemm corner case: always worse than conv_lat
+    if (units >= lat_min) continue;
+    const int nks = (int)op_ks[i].size();
+    if (nks < 2) continue;
+    // only when its 64 x 128 tiles fit one round of workgroups (one per CU): measured on MI355X, a
+    // second round costs more than the halo kernels' under-filled grid (30x40 level at B=32:
+    // 44-50 us vs 24 us), one round wins or ties (15x20 and below, Roots, DLA-34's 27-channel
+    // offset / mask conv at 15x20: 43 vs 98 us)
+    int lmt = 0, lnt = 0;
+    if (lat_units < 0 && conv_lat_tiles(p.M, p.N, &lmt, &lnt) > cu_count) continue;
+    p.weight = packed[i].w;  // [Npad][Kpad] (the halo kernels may have swapped in their own copy)
+    conv_lat_tiles(p.M, p.N, &p.mtiles, &p.ntiles);
+    p.nks = nks;
+    if (!ws->use_pipe[i]) {
+      ks_off[i] = all_ks.size();
+      all_ks.insert(all_ks.end(), op_ks[i].begin(), op_ks[i].end());
+    }
+    ws->use_pipe[i] = 0;
+    ws->c3_tw[i] = 0;
+    ws->s2_grid[i] = 0;
+    ws->lat[i] = 1;
+  }
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
     for (size_t i = 0; i < plan.ops.size(); ++i)
-      if (ws->use_pipe[i]) ws->params[i].ks = ws->dks + ks_off[i];
+      if (ws->use_pipe[i] || ws->lat[i]) ws->params[i].ks = ws->dks + ks_off[i];
   }
   TV_HIP(hipMalloc((void**)&ws->dparams, ws->params.size() * sizeof(ConvParams)));
   TV_HIP(hipMemcpy(ws->dparams, ws->params.data(), ws->params.size() * sizeof(ConvParams), hipMemcpyHostToDevice));
@@ -817,6 +860,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;
   if (ws->small[i]) return launch_conv_small(p, ws->dparams + i, dtype, cu_count, s);
+  if (ws->lat[i]) return launch_conv_lat(p, ws->dparams + i, dtype, s);
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
                                            ws->c3_res[i], ws->c3_ni[i])
@@ -959,6 +1003,8 @@ const char* Engine::op_kernel(int B, size_t i) {
       else if (ws->small[i])
         name = std::string("tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";
+      else if (ws->lat[i])
+        name = std::string("tv::lat::conv_lat<") + t + ">";
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";

@@ -41,6 +41,7 @@ struct Workspace {
   std::vector<int> head_fused;      // per op: 1 = stacked 3x3 heads with the 1x1 heads fused in
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
   std::vector<int> small;           // per op: 1 = narrow-channel 3x3 conv on conv_small.hip
+  std::vector<int> lat;             // per op: 1 = split-K small-level GEMM on conv_lat.hip
   std::vector<int> dcn_skip;        // per op: 1 = DCN sampling done inside the next op's fused kernel
   std::vector<DcnParams> dcn;       // per op: fused DCNv2 launch (dcn.hip) when dcn[i].x != null
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
@@ -70,6 +71,10 @@ struct Engine {
   int headfuse_mode = 1;       // fuse the 1x1 heads into the 3x3 heads epilogue (env TV_HEADFUSE=0 off)
   int convt_mode = 1;          // convt.hip for eligible fp16/bf16 up-paths (env TV_CONVT=0 off)
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
+  int lat_mode = 1;            // conv_lat.hip for layers whose chosen kernel fills < lat_units work units
+                               // (env TV_LAT=0 off)
+  int prio_young = 1;          // halo kernels: s_setprio 1 for waves 4-7 (env TV_PRIO=0 off)
+  int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1
   // concurrent slices: a batch of >= slices * slice_min frames runs as `slices` near-equal parts,

@@ -24,6 +24,7 @@ struct Walker {
   const tv_model_desc& d;
   Plan& P;
   explicit Walker(const tv_model_desc& desc, Plan& plan) : d(desc), P(plan) {}
+  bool backbone_only() const { return d.arch == TV_ARCH_CENTERNET_BACKBONE; }
 
   // ---------------- (1) parameters ----------------
   void add(const std::string& n, std::vector<int64_t> s) { P.params.push_back({n, std::move(s)}); }
@@ -95,7 +96,7 @@ struct Walker {
     std::vector<int> sc;
     for (int i = 1; i < L; ++i) sc.push_back(1 << i);
     ida_p("backbone.ida_up_reverse", fc, sc, true);
-    for (int h = 0; h < d.n_heads; ++h) {
+    for (int h = 0; h < (backbone_only() ? 0 : d.n_heads); ++h) {
       conv_p("heads." + std::to_string(h) + ".0", 2 * ch[0], ch[0], 3);
       conv_p("heads." + std::to_string(h) + ".2", d.head_channels[h], 2 * ch[0], 1);
     }
@@ -255,8 +256,29 @@ struct Walker {
       cur = up_add("backbone.ida_up_reverse", i, collected[i + 1], cur, 1 << (i + 1));
       if (cur < 0) return 2;
     }
-    // heads: stacked 3x3 (C -> 2C each) + LeakyReLU, then block-diagonal 1x1 to fp32 output
     const int C = ch[0];
+    if (backbone_only()) {
+      // DLABackbone.forward's result (dla.py:409-416) into the caller's fp32 NHWC buffer: an
+      // identity 1x1 GEMM (exact: one product per output, fp32 accumulation)
+      const TensorSpec ft = P.tensors[cur];
+      OpSpec o;
+      o.kind = OP_CONV;
+      o.label = "backbone output -> fp32 NHWC";
+      SegSpec sg{cur, "", "", 0, C, 1, 1, 1, 0};
+      sg.identity = true;
+      o.segs = {sg};
+      o.N = C;
+      o.act = 0;
+      o.out = -1;
+      P.out_c = C;
+      P.out_cpad = C;
+      P.out_h = ft.H;
+      P.out_w = ft.W;
+      P.ops.push_back(o);
+      for (auto& op : P.ops) P.flops_per_frame += op.flops;
+      return 0;
+    }
+    // heads: stacked 3x3 (C -> 2C each) + LeakyReLU, then block-diagonal 1x1 to fp32 output
     OpSpec h1;
     h1.kind = OP_CONV;
     h1.label = "heads.*.0 (stacked) + LeakyReLU";
@@ -302,11 +324,12 @@ struct Walker {
 int build_plan(const tv_model_desc& d, Plan* plan) {
   if (d.arch == TV_ARCH_DLA34) return build_plan_dla34(d, plan);
   if (d.arch == TV_ARCH_PROTONET) return build_plan_protonet(d, plan);
-  if (d.arch != TV_ARCH_CENTERNET) {
+  if (d.arch != TV_ARCH_CENTERNET && d.arch != TV_ARCH_CENTERNET_BACKBONE) {
     set_error("unknown model arch");
     return TV_EINVAL;
   }
-  if (d.n_levels < 1 || d.n_levels > 8 || d.downsamples < 0 || d.downsamples > 6 || d.n_heads < 1 ||
+  const bool heads = d.arch == TV_ARCH_CENTERNET;
+  if (d.n_levels < 1 || d.n_levels > 8 || d.downsamples < 0 || d.downsamples > 6 || (heads && d.n_heads < 1) ||
       d.n_heads > 16 || d.in_h < 1 || d.in_w < 1 || d.compute_dtype < 0 || d.compute_dtype > 2) {
     set_error("model desc out of range");
     return TV_EINVAL;
@@ -323,7 +346,7 @@ int build_plan(const tv_model_desc& d, Plan* plan) {
       set_error("backbone_heights out of range");
       return TV_EINVAL;
     }
-  for (int h = 0; h < d.n_heads; ++h)
+  for (int h = 0; heads && h < d.n_heads; ++h)
     if (d.head_channels[h] < 1) {
       set_error("head channel counts must be positive");
       return TV_EINVAL;

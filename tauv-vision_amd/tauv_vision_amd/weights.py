@@ -8,7 +8,7 @@ import torch
 from . import _lib
 
 
-ARCH_CENTERNET, ARCH_DLA34, ARCH_PROTONET = 0, 1, 2
+ARCH_CENTERNET, ARCH_DLA34, ARCH_PROTONET, ARCH_CENTERNET_BACKBONE = 0, 1, 2, 3
 
 
 def model_desc(heights, channels, downsamples, head_channels, in_h=64, in_w=64, precision="fp32",

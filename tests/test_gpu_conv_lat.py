@@ -1,0 +1,68 @@
+"""conv_lat.hip (the small-level latency kernel: small tiles, K split over the waves of a
+workgroup) against the reference goldens.
+
+By default the engine picks conv_lat only for layers its other kernels spread over fewer work
+units than there are CUs (the deep DLA levels). These tests force it onto every eligible layer
+(TV_LAT_UNITS huge) at B = 1 and 3, so 3x3 / stride-2 / Root concatenations / the
+fused 1x1 residual / DLA-34's identity residuals all run through it at full size, and compare
+with the reference outputs at the same tolerances as the default path (test_gpu_forward.py,
+test_gpu_dla34.py).
+"""
+import pytest
+import torch
+
+from helpers import golden, case_input, dla34_input
+
+import test_gpu_dla34 as dla
+import test_gpu_forward as fwd
+
+pytestmark = pytest.mark.gpu
+
+
+def _force(monkeypatch):
+    monkeypatch.setenv("TV_LAT_UNITS", str(10 ** 9))
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("B", [1, 3])
+def test_lat_everywhere_r18_full_size(monkeypatch, precision, B):
+    _force(monkeypatch)
+    name = "r18_c128_b1_480x640"
+    model, oc, mc, case = fwd.build(name, precision)
+    eng = model.engine(torch.device("cuda", 0), 480, 640)
+    frames = torch.zeros((B, 480, 640, 3), dtype=torch.uint8, device="cuda")
+    kern = {label: k for label, _, _, k in eng.profile(frames, eng.alloc_out(B))}
+    n_lat = sum(k.startswith("tv::lat::conv_lat<") for k in kern.values())
+    assert n_lat >= 60, kern  # every 128-channel conv but the stem and the fused heads
+    img = case_input(name).cuda()
+    # the golden frame at the last batch position (M not a multiple of the 64-pixel tile)
+    pred = model(torch.cat([torch.flip(img, [-1])] * (B - 1) + [img], 0))
+    g = golden(f"model_{name}")
+    for f in ("heatmap", "size", "offset"):
+        ref = g[f]
+        got = getattr(pred, f)[B - 1:].detach().cpu().numpy()
+        scale = max(1.0, float(abs(ref).max()))
+        assert float(abs(got - ref).max()) <= fwd.TOL[precision] * scale, f
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_lat_everywhere_dla34(monkeypatch, precision):
+    _force(monkeypatch)
+    name = "b1_480x640_kp"
+    model, oc, mc, case = dla.build(name, precision)
+    pred = model(dla34_input(name).cuda())
+    dla._cmp(pred, golden(f"dla34_{name}"), dla.TOL[precision])
+
+
+def test_lat_default_selection_b32():
+    """At the bench's 32-frame slice the deep levels (30x40 and below) run on conv_lat and the
+    120x160 / 60x80 levels stay on the halo kernels."""
+    name = "r18_c128_b1_480x640"
+    model, oc, mc, case = fwd.build(name, "fp16")
+    eng = model.engine(torch.device("cuda", 0), 480, 640)
+    frames = torch.zeros((32, 480, 640, 3), dtype=torch.uint8, device="cuda")
+    kern = {label: k for label, _, _, k in eng.profile(frames, eng.alloc_out(32))}
+    assert kern["backbone.dla_down.tree_layers.2.tree_l.tree_r.conv1"].startswith("tv::lat::conv_lat<"), kern
+    assert kern["backbone.dla_down.tree_layers.4.tree_r.root.conv"].startswith("tv::lat::conv_lat<"), kern
+    assert kern["backbone.dla_down.tree_layers.0.tree_l.tree_r.conv1"].startswith("tv::c3::conv3x3<"), kern
+    assert kern["backbone.multi_ida_up.ida_up_layers.0.output_layers.0.0"].startswith("tv::c3::conv3x3<"), kern

@@ -54,6 +54,22 @@ def test_flops_match_survey():
     assert abs(g["flops_per_frame"] / 1e9 - 220.19) < 0.01
 
 
+@pytest.mark.parametrize("name", list(models_index()))
+def test_backbone_only_layout_and_geometry(name):
+    """TV_ARCH_CENTERNET_BACKBONE (standalone DLABackbone.forward): exactly the "backbone.*" keys of
+    the full network in the same order, output = channels[0] at in / 2^downsamples."""
+    from tauv_vision_amd.weights import ARCH_CENTERNET_BACKBONE, model_desc, param_layout, geometry
+    case = case_by_name(name)
+    full = param_layout(_desc_for(case))
+    d = model_desc(case["heights"], case["channels"], case["downsamples"], [1], case["in_h"], case["in_w"],
+                   "fp32", arch=ARCH_CENTERNET_BACKBONE)
+    assert param_layout(d) == [(k, s) for k, s in full if k.startswith("backbone.")]
+    g = geometry(d)
+    ds = case["downsamples"]
+    assert (g["out_h"], g["out_w"], g["out_channels"], g["out_cpad"]) == (
+        case["in_h"] >> ds, case["in_w"] >> ds, case["channels"][0], case["channels"][0])
+
+
 def test_bad_desc_rejected():
     from tauv_vision_amd.weights import model_desc, geometry
     with pytest.raises(RuntimeError):  # TV_ESHAPE: channels not a multiple of the 16-byte vector

@@ -10,7 +10,7 @@ Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may
 import it, and only as the checker / the timed CPU baseline. The product path
 (`tauv-vision_amd/`) never imports it and has no CPU fallback.
 """
-from .ref_forward import centernet_forward, pad_to_match, head_channels_for, PredictionRef  # noqa: F401
+from .ref_forward import centernet_forward, backbone_forward, pad_to_match, head_channels_for, PredictionRef  # noqa: F401
 from .ref_decode import (heatmap_nms, heatmap_detect, decode, decode_keypoints,  # noqa: F401
                          depth_decode)
 from .ref_preprocess import preprocess  # noqa: F401

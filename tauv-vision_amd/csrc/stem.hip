@@ -66,7 +66,9 @@ template <> struct Window<0> { static constexpr int NS = (NVAL + NT - 1) / NT; }
 template <> struct Window<1> { static constexpr int NS = (NVAL + NT - 1) / NT; };
 template <> struct Window<2> { static constexpr int NS = (RR * 30 + NT - 1) / NT; };  // 2 dwords per thread
 
-template <typename T, int MODE>
+// NI: 32-channel output blocks computed (4 for C0 = 128; 1 for DLA-34's 16-channel base layer,
+// whose tiles would otherwise spend 3/4 of their MFMAs and epilogue on padding channels)
+template <typename T, int MODE, int NI>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void stem_conv(
     StemParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -219,18 +221,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto mfma_row = [&](int ebuf, auto fc) __attribute__((always_inline)) {
     constexpr int f = decltype(fc)::value;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[f][i] = f32x16{};
+    for (int i = 0; i < NI; ++i) acc[f][i] = f32x16{};
 #pragma unroll
     for (int j = 0; j < KS; ++j) {
       const int c0 = 2 * j;  // lane half 0's chunk
       const int off0 = (c0 / 3) * TW * EPIX + (c0 % 3) * 16 + ebuf * EBUF;
       const char* base = j == KS - 1 ? ab0 : (c0 % 3 == 2 ? abrow : ab16);
-      uint4 b[4];
+      uint4 b[NI];
       const uint4 a = *reinterpret_cast<const uint4*>(base + off0 + f * TW * EPIX);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) b[i] = *reinterpret_cast<const uint4*>(wfl + (j * 4 + i) * 1024);
+      for (int i = 0; i < NI; ++i) b[i] = *reinterpret_cast<const uint4*>(wfl + (j * 4 + i) * 1024);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Mfma<T>::run(b[i], a, acc[f][i]);
+      for (int i = 0; i < NI; ++i) Mfma<T>::run(b[i], a, acc[f][i]);
     }
   };
 
@@ -246,7 +248,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       const bool ok = y < H && x < W;
       T* dst = reinterpret_cast<T*>(p.out) + ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.out_ldc;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NI; ++i) {
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
           float v[2][4];
@@ -298,10 +300,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, int NI>
 static int launch_t(const StemParams& p, int grid, hipStream_t s) {
-  auto k = stem_conv<T, MODE>;
-  if (int r = ensure_lds<stem_conv<T, MODE>>(LDS)) return r;
+  auto k = stem_conv<T, MODE, NI>;
+  if (int r = ensure_lds<stem_conv<T, MODE, NI>>(LDS)) return r;
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), LDS, s, p);
   TV_HIP(hipGetLastError());
   return 0;
@@ -332,10 +334,15 @@ int launch_stem(const StemParams& p, int dtype, int grid, hipStream_t s) {
   if (grid > ntot) grid = (int)ntot;
   const int mode = p.u8 ? (p.W % 4 == 0 ? 2 : 1) : 0;
   using L = int (*)(const StemParams&, int, hipStream_t);
-  static const L f16[3] = {stem::launch_t<_Float16, 0>, stem::launch_t<_Float16, 1>, stem::launch_t<_Float16, 2>};
-  static const L b16[3] = {stem::launch_t<__bf16, 0>, stem::launch_t<__bf16, 1>, stem::launch_t<__bf16, 2>};
-  if (dtype == F16) return f16[mode](p, grid, s);
-  if (dtype == BF16) return b16[mode](p, grid, s);
+  static const L f16[2][3] = {
+      {stem::launch_t<_Float16, 0, 4>, stem::launch_t<_Float16, 1, 4>, stem::launch_t<_Float16, 2, 4>},
+      {stem::launch_t<_Float16, 0, 1>, stem::launch_t<_Float16, 1, 1>, stem::launch_t<_Float16, 2, 1>}};
+  static const L b16[2][3] = {
+      {stem::launch_t<__bf16, 0, 4>, stem::launch_t<__bf16, 1, 4>, stem::launch_t<__bf16, 2, 4>},
+      {stem::launch_t<__bf16, 0, 1>, stem::launch_t<__bf16, 1, 1>, stem::launch_t<__bf16, 2, 1>}};
+  const int narrow = p.N <= 32 ? 1 : 0;
+  if (dtype == F16) return f16[narrow][mode](p, grid, s);
+  if (dtype == BF16) return b16[narrow][mode](p, grid, s);
   set_error("stem: fp16/bf16 only");
   return 1;
 }

@@ -253,7 +253,9 @@ def test_gpu_protonet_matches_reference(name, precision):
 @pytest.mark.gpu
 def test_gpu_protonet_batch_consistency():
     """Frames are independent: a batch (incl. the two concurrent slices of B >= 16) gives every
-    frame exactly its single-frame result."""
+    frame its single-frame result — within fp16 rounding, since the kernel choice may depend on
+    the batch (the split-K conv_lat for layers a small batch leaves under-filled sums K in
+    another order) — and a repeated run of the same batch is bit-identical."""
     from tauv_vision_amd.yolact import Masknet, YolactConfig
     c = protonet_case("protonet_f64_k16_b1_9x17")
     sd, _ = protonet_inputs(c)
@@ -261,5 +263,7 @@ def test_gpu_protonet_batch_consistency():
     m.load_state_dict(sd)
     x = torch.randn(17, 64, 9, 17, generator=torch.Generator().manual_seed(4)).cuda()
     yb = m(x).cpu()
+    np.testing.assert_array_equal(m(x).cpu().numpy(), yb.numpy())
+    scale = max(1.0, float(yb.abs().max()))
     for i in (0, 8, 16):
-        np.testing.assert_array_equal(m(x[i:i + 1]).cpu().numpy(), yb[i:i + 1].numpy())
+        np.testing.assert_allclose(m(x[i:i + 1]).cpu().numpy(), yb[i:i + 1].numpy(), rtol=0, atol=1e-3 * scale)

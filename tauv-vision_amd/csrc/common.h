@@ -89,7 +89,6 @@ struct ConvParams {
   const float* head_b;  // [ntiles][32] 1x1 bias on the first tile of each head, zeros elsewhere
   int head_ldc;
   int head_row0[16], head_nrows[16];
-  int flags;            // halo kernels: bit 0 = static s_setprio 1 for the younger half (waves 4-7)
 };
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.

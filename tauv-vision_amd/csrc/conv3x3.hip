@@ -17,7 +17,8 @@ __global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntil
     const int chunk = slot ^ ((row >> 2) & 3);
     const int cb = q / (9 + res), tap = q - cb * (9 + res);
     const int k16 = (tap * CBK * ncb + cb * CBK) / 8 + chunk;  // 16-byte column (8 elements); tap 9 = residual
-    out[o] = w[(size_t)(nt * bnk + row) * kpad16 + k16];
+    // (residual blocks past a narrower residual segment: zero weights, past Kpad included)
+    out[o] = k16 < kpad16 ? w[(size_t)(nt * bnk + row) * kpad16 + k16] : make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -33,7 +34,7 @@ size_t conv3x3_weight_bytes(int ntiles, int res, int ncb) {
 }
 
 int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, void* out, hipStream_t s) {
-  if ((Kpad * esz) % 16 || Kpad < (9 + res) * 32 * ncb || (ni != 4 && ni != 2) || (ncb != 2 && ncb != 4 && ncb != 8)) {
+  if ((Kpad * esz) % 16 || Kpad < (9 * ncb + res) * 32 || (ni != 4 && ni != 2) || (ncb != 2 && ncb != 4 && ncb != 8)) {
     set_error("conv3x3_repack: bad Kpad / ni / channel blocks");
     return 1;
   }

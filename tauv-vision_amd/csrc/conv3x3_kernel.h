@@ -192,10 +192,6 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int ntl = first < end ? UP * ((end - first + stride - 1) / stride) : 0;
   if (ntl == 0) return;
   const int S_tot = ntl * SPTK;
-  // the second-dispatched half of the workgroup loses VALU / issue arbitration to the older
-  // half on every segment; one static priority raise (no per-segment flips) evens it out
-  if (p.flags & 1)
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 
   // bias of every output channel into LDS (read in the epilogues)
   float* lbias = reinterpret_cast<float*>(smem + OFF_B);
@@ -292,7 +288,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     rs.w = 0x00020000;
     const int q = (int)(rgeo[i] >> 2), c = (int)(rgeo[i] & 3);
     const int y = y0 + q / TW, x = x0 + q % TW;
-    const bool ok = y < H && x < W && fr < nframes;  // a phantom unit's frame is past the tensor: OOB zeros
+    // a phantom unit's frame is past the tensor, and a residual input narrower than the 3x3 input
+    // (DLA-34 Tree's 1x1 `project` of the pooled bottom: C / 2 channels) has no block cb: OOB zeros
+    const bool ok = y < H && x < W && fr < nframes && cb * CBK < sr.C;
     const unsigned off = ok ? ((unsigned)(y * sr.stride) * (unsigned)sr.W + (unsigned)(x * sr.stride)) * rpix_bytes +
                                   (unsigned)c * 16u
                             : 0x80000000u;

@@ -298,7 +298,6 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_LAT")) lat_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_LAT_UNITS")) lat_units = std::atoi(env);
-  if (const char* env = std::getenv("TV_PRIO")) prio_young = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
@@ -524,14 +523,15 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.mtiles = mt;
     }
     p.zero = zero_page;
-    p.flags = prio_young ? 1 : 0;
     // persistent halo-tile 3x3 kernel (conv3x3.hip): 3x3 / stride 1 / pad 1, one input of 128
     // channels, fp16/bf16, 16-byte aligned channel slices, byte offsets within 2^31
     // A second segment is accepted when it is ResidualBlock's 1x1 conv_residual (128 channels,
     // stride 1 or 2, ReLU after the sum): one extra k-step per channel block (RES).
     // (or DLA-34 BasicBlock's identity residual: 64 / 128 / 256 channels, an identity 1x1)
+    // (a residual narrower than the 3x3 input — DLA-34 Tree's `project` of the pooled bottom, C/2
+    // channels — reads zeros with zero weights in its missing channel blocks)
     const bool res2 = op.segs.size() == 2 && op.segs[1].kh == 1 && op.segs[1].kw == 1 && op.segs[1].pad == 0 &&
-                      p.seg[1].C == p.seg[0].C && p.seg[1].ldc % 8 == 0 && p.N == p.seg[1].C && op.act == 1 &&
+                      p.seg[1].C <= p.seg[0].C && p.seg[1].C % 32 == 0 && p.seg[1].ldc % 8 == 0 && op.act == 1 &&
                       (size_t)p.seg[1].H * p.seg[1].W * p.seg[1].ldc * esz < (1ull << 31) &&
                       p.seg[1].H >= (p.Ho - 1) * p.seg[1].stride + 1 && p.seg[1].W >= (p.Wo - 1) * p.seg[1].stride + 1;
     if (conv3_mode && dtype != F32 && op.kind == OP_CONV && (op.segs.size() == 1 || res2) && op.out >= 0 &&
@@ -982,9 +982,11 @@ const char* Engine::op_kernel(int B, size_t i) {
     const OpSpec& op = plan.ops[i];
     if (op.kind == OP_PREP) return stem_op >= 0 ? "prep (fused into the stem)" : "prep";
     if ((int)i == stem_op) {
-      static const char* sn[2][2] = {{"tv::stem::stem_conv<_Float16, false>", "tv::stem::stem_conv<_Float16, true>"},
-                                     {"tv::stem::stem_conv<__bf16, false>", "tv::stem::stem_conv<__bf16, true>"}};
-      return sn[dtype == BF16][profiled_u8 ? 1 : 0];
+      std::string& name = ws->kname[i];  // (input kind of the last profile(): rebuilt per call)
+      const int smode = profiled_u8 ? (desc.in_w % 4 == 0 ? 2 : 1) : 0;
+      name = std::string("tv::stem::stem_conv<") + tn[dtype] + ", " + std::to_string(smode) + ", " +
+             (plan.ops[i].N <= 32 ? "1" : "4") + ">";
+      return name.c_str();
     }
     if (op.kind == OP_LAYOUT_IN) return dtype == F32 ? "tv::nchw_to_nhwc<float>" : dtype == F16 ? "tv::nchw_to_nhwc<_Float16>" : "tv::nchw_to_nhwc<__bf16>";
     const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;

@@ -73,7 +73,6 @@ struct Engine {
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
   int lat_mode = 1;            // conv_lat.hip for layers whose chosen kernel fills < lat_units work units
                                // (env TV_LAT=0 off)
-  int prio_young = 1;          // halo kernels: s_setprio 1 for waves 4-7 (env TV_PRIO=0 off)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1

@@ -145,7 +145,7 @@ struct DcnParams {
   int out_ldc, N;
 };
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad);
-int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s);
+int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, hipStream_t s);  // dcn64_mode: 64-channel k-steps when C % 64 == 0
 
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
 // output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC

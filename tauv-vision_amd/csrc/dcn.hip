@@ -256,6 +256,245 @@ __global__ __launch_bounds__(NT) void dcn_gemm(const DcnParams p) {
     }
 }
 
+
+// ---- 64-channel k-steps (C % 64 == 0, every DLA-34 DeformConv): full-line gathers.
+// The kernel above gives a thread 16 channels of ONE pixel, so each corner-load instruction
+// touches 32 pixels' rows for 32 B each: measured, its gathers run at ~12 TB/s of useful bytes,
+// a quarter of the L1 lines they touch. Here a k-step is one tap x 64 channels and a thread owns
+// one 16-byte channel chunk c = tid % 8 of 4 pixels g + 32 j (g = tid / 8): the 8 lanes of a
+// pixel read its 128-byte corner row together, so an instruction fetches 8 whole lines. The
+// per-(pixel, tap) sampling state (4 corner offsets, 4 mask-folded weights) is computed once by
+// thread p < 128 two taps ahead into an LDS ring of 3 taps and read by the pixel's 8 lanes
+// (broadcast). Same blend arithmetic and the same K order as dcn_gemm: the results are identical.
+// LDS rows of 128 B (64 K values), 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7)
+// (conflict-free fragment reads without padding: two workgroups per CU fit)
+constexpr int ROW2 = 128;
+__device__ __forceinline__ int sw2(int r, int c) { return r * ROW2 + ((c ^ ((r >> 1) & 7)) << 4); }
+// PX pixels per workgroup (128, or 64: half the registers and LDS, twice the resident workgroups
+// to hide the corner gathers' latency on layers whose MFMA work per k-step is small)
+template <int PX> constexpr int abuf2() { return PX * ROW2; }
+template <int BN> constexpr int wbuf2() { return BN * ROW2; }
+template <int PX> constexpr int pslot() { return PX * 32; }  // one tap's sampling state: (4 int + 4 float) per pixel
+template <int BN, int PX> constexpr int lds_bytes2() { return 2 * (abuf2<PX>() + wbuf2<BN>()) + 3 * pslot<PX>(); }
+
+template <typename T, int BN, int PX>
+__global__ __launch_bounds__(NT, PX == 64 ? (BN == 64 ? 4 : 3) : 2) void dcn_gemm64(const DcnParams p) {
+  constexpr int PJ = PX / 32;            // pixels per thread per k-step
+  constexpr int WPX = PX / 32;           // waves along pixels (32 each); the rest split the channels
+  constexpr int NA = BN / 32 / (4 / WPX);  // 32-channel accumulator blocks per wave
+  constexpr int WBUF = wbuf2<BN>();
+  constexpr int ABUF2 = abuf2<PX>();
+  constexpr int PSLOT = pslot<PX>();
+  constexpr int WCH = BN * 8 / NT;       // 16-byte weight chunks per thread per k-step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const Pring = smem + 2 * (ABUF2 + WBUF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int HW = p.H * p.W;
+  const int M = p.B * HW;
+  const int G = gridDim.x, ny = p.N / BN;
+  const int q = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int m0 = (q / ny) * PX, n0 = (q % ny) * BN;
+  const int ncb = p.C / 64;
+  const int S = 9 * ncb;
+
+  i32x4 xr, wrs;
+  {
+    const unsigned long long a = (unsigned long long)p.x, aw = (unsigned long long)p.w;
+    xr = i32x4{(int)(unsigned)a, (int)(unsigned)(a >> 32), (int)((unsigned)M * p.ldx * (unsigned)sizeof(T)), 0x00020000};
+    wrs = i32x4{(int)(unsigned)aw, (int)(unsigned)(aw >> 32), (int)((unsigned)p.N * p.Kpad * (unsigned)sizeof(T)),
+                0x00020000};
+  }
+
+  // ---- sampling-state producer: thread tid < PX owns pixel tid (dcn_sample's expressions)
+  const int pm = m0 + (tid & (PX - 1));
+  const bool pval = tid < PX && pm < M;
+  const int pb = pval ? pm / HW : 0;
+  const int prem = pval ? pm - pb * HW : 0;
+  const int poy = prem / p.W, pox = prem - (prem / p.W) * p.W;
+  const T* om = reinterpret_cast<const T*>(p.om) + (size_t)(pval ? pm : 0) * p.om_ldc;
+  float nom[3] = {0.f, 0.f, 0.f};  // om values of the next tap_state call's tap (loaded one call ahead)
+  auto load_om = [&](int k) __attribute__((always_inline)) {
+    if (pval) {
+      nom[0] = (float)om[2 * k];
+      nom[1] = (float)om[2 * k + 1];
+      nom[2] = (float)om[18 + k];
+    }
+  };
+  auto tap_state = [&](int k) __attribute__((always_inline)) {
+    // om values of tap k -> 4 corner byte offsets of the pixel (kOOB: outside) + weights x mask
+    int vo[4] = {kOOB, kOOB, kOOB, kOOB};
+    float wt[4] = {0.f, 0.f, 0.f, 0.f};
+    const float dy = nom[0], dx = nom[1], logit = nom[2];
+    if (k + 1 < 9) load_om(k + 1);
+    if (pval) {
+      const float mask = 1.0f / (1.0f + expf(-logit));
+      const float py = (float)(poy - 1 + k / 3) + dy;
+      const float px = (float)(pox - 1 + k % 3) + dx;
+      if (py > -1.f && py < (float)p.H && px > -1.f && px < (float)p.W) {
+        const float fy = floorf(py), fx = floorf(px);
+        const int y0 = (int)fy, x0 = (int)fx;
+        const float ly = py - fy, lx = px - fx, hy = 1.f - ly, hx = 1.f - lx;
+        const float w4[4] = {hy * hx, hy * lx, ly * hx, ly * lx};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int yy = y0 + (c >> 1), xx = x0 + (c & 1);
+          if (yy >= 0 && yy <= p.H - 1 && xx >= 0 && xx <= p.W - 1) {
+            vo[c] = ((pb * HW + yy * p.W + xx) * p.ldx) * (int)sizeof(T);
+            wt[c] = w4[c] * mask;
+          }
+        }
+      }
+    }
+    if (tid < PX) {
+      int* d = reinterpret_cast<int*>(Pring + (k % 3) * PSLOT + tid * 32);
+      *reinterpret_cast<int4*>(d) = make_int4(vo[0], vo[1], vo[2], vo[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(wt[0], wt[1], wt[2], wt[3]);
+    }
+  };
+
+  // ---- gather geometry: chunk c of pixels g + 32 j
+  const int gc = tid & 7, gg = tid >> 3;
+  int voff[PJ][4];
+  float wts[PJ][4];
+  auto read_state = [&](int k) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const int* d = reinterpret_cast<const int*>(Pring + (k % 3) * PSLOT + (gg + 32 * j) * 32);
+      const int4 o = *reinterpret_cast<const int4*>(d);
+      const float4 w = *reinterpret_cast<const float4*>(d + 4);
+      voff[j][0] = o.x + 16 * gc; voff[j][1] = o.y + 16 * gc; voff[j][2] = o.z + 16 * gc; voff[j][3] = o.w + 16 * gc;
+      wts[j][0] = w.x; wts[j][1] = w.y; wts[j][2] = w.z; wts[j][3] = w.w;
+    }
+  };
+  uint4 cv[PJ][4];  // [pixel j][corner]
+  auto load_corners = [&](int cb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PJ; ++j)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) cv[j][c] = to_u4(raw_buffer_load_v4(xr, voff[j][c], cb * 64 * (int)sizeof(T), 0));
+  };
+  // weights of k-step s: chunk i of this thread = row (tid + NT i) / 8, 16-byte column (tid % 8)
+  uint4 wv[WCH];
+  auto load_w = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int r = (tid + NT * i) >> 3;
+      wv[i] = to_u4(raw_buffer_load_v4(wrs, ((n0 + r) * p.Kpad + 8 * gc) * (int)sizeof(T), s * 64 * (int)sizeof(T), 0));
+    }
+  };
+  auto produce = [&](int s) __attribute__((always_inline)) {
+    char* A = smem + (s & 1) * (ABUF2 + WBUF);
+    char* Wl = A + ABUF2;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      unsigned o[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        float a0, a1;
+        if constexpr (std::is_same<T, _Float16>::value) {
+          const unsigned d0 = reinterpret_cast<const unsigned*>(&cv[j][0])[e >> 1];
+          a0 = mix_lo(wts[j][0], d0);
+          a1 = mix_hi(wts[j][0], d0);
+#pragma unroll
+          for (int c = 1; c < 4; ++c) {
+            const unsigned dw = reinterpret_cast<const unsigned*>(&cv[j][c])[e >> 1];
+            a0 = mix_lo_acc(wts[j][c], dw, a0);
+            a1 = mix_hi_acc(wts[j][c], dw, a1);
+          }
+        } else {
+          a0 = 0.f;
+          a1 = 0.f;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            a0 += wts[j][c] * elem<T>(cv[j][c], e);
+            a1 += wts[j][c] * elem<T>(cv[j][c], e + 1);
+          }
+        }
+        o[e >> 1] = pack2<T>(a0, a1);
+      }
+      *reinterpret_cast<uint4*>(A + sw2(gg + 32 * j, gc)) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) *reinterpret_cast<uint4*>(Wl + sw2((tid + NT * i) >> 3, gc)) = wv[i];
+  };
+
+  f32x16 acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = f32x16{};
+  // wave (wp, wc): pixels 32 wp .. + 31 x accumulator blocks wc * NA .. + NA - 1
+  const int wp = wave % WPX, wc = wave / WPX;
+  auto consume = [&](int s) __attribute__((always_inline)) {
+    const char* A = smem + (s & 1) * (ABUF2 + WBUF);
+    const char* Wl = A + ABUF2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // four 16-deep sub-steps
+      const uint4 xf = *reinterpret_cast<const uint4*>(A + sw2(32 * wp + l32, 2 * j + lh));
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const uint4 wf = *reinterpret_cast<const uint4*>(Wl + sw2(32 * (wc * NA + i) + l32, 2 * j + lh));
+        Mfma<T>::run(wf, xf, acc[i]);
+      }
+    }
+  };
+
+  // ---- pipeline: sampling state of taps 0 and 1, then step 0's operands. Tap k's state is
+  // written at the first step of tap k - 2 (slot k % 3, last read when tap k - 3's state was
+  // consumed, a barrier or more earlier) and read when step 0 of tap k is issued (the last step
+  // of tap k - 1: at least one barrier after it was written).
+  load_om(0);
+  tap_state(0);
+  tap_state(1);
+  load_w(0);
+  __syncthreads();
+  read_state(0);
+  load_corners(0);
+  for (int s = 0; s < S; ++s) {
+    const int k = s / ncb, cb = s - k * ncb;
+    produce(s);  // blends step s's corners into LDS buffer s & 1
+    if (cb == 0 && k + 2 < 9) tap_state(k + 2);
+    const int s1 = s + 1;
+    if (s1 < S) {
+      const int k1 = s1 / ncb, cb1 = s1 - k1 * ncb;
+      if (cb1 == 0) read_state(k1);
+      load_corners(cb1);
+      load_w(s1);
+    }
+    __syncthreads();  // buffer s & 1 complete; every wave's reads of buffer (s - 1) & 1 are done
+    consume(s);
+  }
+
+  // ---- epilogue (as dcn_gemm)
+  const int mo = m0 + 32 * wp + l32;
+  if (mo >= M) return;
+  T* dst = reinterpret_cast<T*>(p.out) + (size_t)mo * p.out_ldc + n0;
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = 32 * (wc * NA + i) + 8 * g + 4 * lh;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc[i][4 * g + e] + p.bias[n0 + ch + e];
+        if (p.act == 1) t = fmaxf(t, 0.0f);
+        else if (p.act == 2) t = fmaxf(t, 0.01f * t);
+        v[e] = t;
+      }
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(dst + ch) = u32x2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+    }
+}
+
+template <typename T, int BN, int PX>
+static void launch64(const DcnParams& p, hipStream_t s) {
+  constexpr int lds = lds_bytes2<BN, PX>();
+  (void)ensure_lds<dcn_gemm64<T, BN, PX>>(lds);
+  const long M = (long)p.B * p.H * p.W;
+  const dim3 grid((unsigned)((M + PX - 1) / PX * (p.N / BN)));
+  hipLaunchKernelGGL((dcn_gemm64<T, BN, PX>), grid, dim3(NT), lds, s, p);
+}
+
 }  // namespace dcn
 
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad) {
@@ -264,7 +503,7 @@ bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, 
   return C % dcn::KS == 0 && N % 64 == 0 && ldx % 8 == 0 && om_ldc >= 27 && out_ldc % 4 == 0;
 }
 
-int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s) {
+int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, hipStream_t s) {
   if (!dcn_gemm_supported((long)p.B * p.H * p.W, p.C, p.N, p.ldx, p.om_ldc, p.out_ldc, p.Kpad) || p.Kpad < 9 * p.C) {
     set_error("dcn_gemm: channels must be multiples of 32 (input) / 64 (output), tensors below 2 GB");
     return 1;
@@ -277,7 +516,20 @@ int launch_dcn_gemm(const DcnParams& p, int dtype, hipStream_t s) {
     set_error("dcn_gemm: fp16/bf16 only");
     return 1;
   }
-  if (dtype == F16) {
+  if (p.C % 64 == 0 && dcn64_mode) {  // full-line gathers (every DLA-34 DeformConv); mode 2: 64-pixel tiles
+    // 64-pixel tiles (measured: 4 resident workgroups per CU hide the corner gathers better than
+    // 2 of 128 pixels; the 64-channel layers 5561 -> 5775 frames/s at B=64); 128-channel outputs
+    // too when 128-pixel tiles would leave few workgroups per CU (B=1: 1.65 -> 1.52 ms; B=64 neutral)
+    const long tiles128 = (M + 127) / 128 * (p.N / 128);
+    const bool px64w = dcn64_mode == 2 || tiles128 < 1024;
+    if (dtype == F16) {
+      if (wide) px64w ? dcn::launch64<_Float16, 128, 64>(p, s) : dcn::launch64<_Float16, 128, 128>(p, s);
+      else dcn::launch64<_Float16, 64, 64>(p, s);
+    } else {
+      if (wide) px64w ? dcn::launch64<__bf16, 128, 64>(p, s) : dcn::launch64<__bf16, 128, 128>(p, s);
+      else dcn::launch64<__bf16, 64, 64>(p, s);
+    }
+  } else if (dtype == F16) {
     if (wide) hipLaunchKernelGGL((dcn::dcn_gemm<_Float16, 128>), grid, dim3(dcn::NT), dcn::lds_bytes<128>(), s, p);
     else hipLaunchKernelGGL((dcn::dcn_gemm<_Float16, 64>), grid, dim3(dcn::NT), dcn::lds_bytes<64>(), s, p);
   } else {

@@ -298,6 +298,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_LAT")) lat_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_LAT_UNITS")) lat_units = std::atoi(env);
+  if (const char* env = std::getenv("TV_DCN64")) dcn64_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
   if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
@@ -825,7 +826,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
                     : launch_prep_nchw((const float*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s);
   }
   if (ws->dcn_skip[i]) return TV_OK;  // sampled inside the next op's fused DCNv2 kernel
-  if (ws->dcn[i].x) return launch_dcn_gemm(ws->dcn[i], dtype, s);
+  if (ws->dcn[i].x) return launch_dcn_gemm(ws->dcn[i], dtype, dcn64_mode, s);
   if (op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_DWCONVT_ADD) {
     const TensorSpec& src = plan.tensors[op.src];
     const TensorSpec& dst = plan.tensors[op.out];
@@ -1001,7 +1002,8 @@ const char* Engine::op_kernel(int B, size_t i) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->dcn_skip[i]) name = "(sampled inside the fused DCNv2 kernel)";
-      else if (ws->dcn[i].x) name = std::string("tv::dcn::dcn_gemm<") + t + (ws->dcn[i].N % 128 == 0 ? ", 128>" : ", 64>");
+      else if (ws->dcn[i].x) name = std::string(dcn64_mode && ws->dcn[i].C % 64 == 0 ? "tv::dcn::dcn_gemm64<" : "tv::dcn::dcn_gemm<") + t +
+               (ws->dcn[i].N % 128 == 0 ? ", 128>" : ", 64>");
       else if (ws->small[i])
         name = std::string("tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";

@@ -73,6 +73,7 @@ struct Engine {
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
   int lat_mode = 1;            // conv_lat.hip for layers whose chosen kernel fills < lat_units work units
                                // (env TV_LAT=0 off)
+  int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (env TV_DCN64=0 off)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1

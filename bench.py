@@ -171,7 +171,9 @@ def conv_roofline(pipe, frames, precision, reps=3):
     top = sorted(best, key=lambda o: -o[1])[:6]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
-            "traffic": load_traffic(name, bs, precision),
+            # the PMC profile is of one pipe.B-frame forward (its launches are the same per-slice
+            # launches timed here), so it is looked up by the forward batch
+            "traffic": load_traffic(name, pipe.B, precision),
             "launch_batch": bs,
             "kernel": f"{name}: {n} launches/forward, avg {ms / n:.4f} ms, avg {flops / n / 1e9:.2f} GFLOP/launch",
             "all_conv": {"launches": len(conv), "ms": round(all_ms, 3), "tflops": round(all_fl / all_ms / 1e9, 1)},

@@ -65,9 +65,13 @@ constexpr int OFF_B = OFF_W + RING * WSLOT;
 constexpr int OFF_R = OFF_B + kConv3MaxN * 4;  // RES: one channel block of the residual input
 constexpr int RBUF = 512 * 64;                  // 512 pixels x 32 channels (XOR-swizzled 16 B chunks)
 constexpr int RPW = RBUF / 1024 / NW;           // residual pieces per wave per channel block = 4
-template <int RES>
-constexpr int lds_bytes() { return OFF_R + (RES ? RBUF : 0); }
-static_assert(lds_bytes<1>() <= 160 * 1024, "LDS budget");
+// EPI 1 (fused 1x1 heads, never RES): the heads' A-fragments of a channel tile (8 k-steps x 64
+// lanes x 16 B) staged by LDS-DMA into one of two buffers in the RES region, one 1 KiB piece per wave
+constexpr int OFF_HW = OFF_R;
+constexpr int HWB = 8 * 1024;
+template <int RES, int EPI = 0>
+constexpr int lds_bytes() { return OFF_R + (RES ? RBUF : EPI ? 2 * HWB : 0); }
+static_assert(lds_bytes<1>() <= 160 * 1024 && lds_bytes<0, 1>() <= 160 * 1024, "LDS budget");
 static_assert(WSLOT / 1024 == NW, "one weight piece per wave per k-step");
 static_assert(HPIECES * 64 >= HPIX * 5, "halo pieces");
 
@@ -142,6 +146,7 @@ template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI, 
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
   static_assert(NI == 4 || (NI == 2 && EPI == 0), "half tiles: plain epilogue only");
+  static_assert(!(EPI == 1 && RES), "fused heads use the residual LDS region for their 1x1 weights");
   constexpr int SPTK = spt<RES, NCB>();  // k-steps per tile
   constexpr int BNK = 32 * NI;      // output channels per tile
   constexpr int WSL = BNK * 64;     // weight bytes per k-step (an LDS ring slot holds up to WSLOT)
@@ -262,6 +267,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
                         cb * CBK * (int)sizeof(T), 0, 0);
   };
 
+  // EPI 1: this wave's 1 KiB piece (k-step `wave` of the 1x1 heads) of channel tile nt's A-fragments
+  [[maybe_unused]] auto head_piece = [&](int nt, int hsel) __attribute__((always_inline)) {
+    dma16(reinterpret_cast<const char*>(p.head_w) + ((size_t)(nt * 8 + wave) * 64 + lane) * 16,
+          lds + OFF_HW + hsel * HWB + wave * 1024);
+  };
+
   // ---- RES: the ResidualBlock's 1x1 conv_residual (dla.py:32-37), or DLA-34 BasicBlock's identity
   // residual (centerpoint_dla.py:30-59, an identity 1x1), as a 10th k-step per channel block. Its input x (second segment, stride rstr) for the tile's 512 output pixels
   // moves into one 32 KiB LDS buffer per channel block: chunk L = piece*64 + lane holds pixel
@@ -369,7 +380,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   // ---- epilogue of the tile (fr, y0, x0, nt): straight from the accumulators
-  auto epilogue = [&](int fr, int y0, int x0, int nt) __attribute__((always_inline)) {
+  auto epilogue = [&](int fr, int y0, int x0, int nt, int hsel) __attribute__((always_inline)) {
     const int n0 = nt * BNK;
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -425,8 +436,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
             const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
             const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
             const uint4 hv = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-            const uint4 hwf = gload16(reinterpret_cast<const char*>(p.head_w) +
-                                      ((size_t)(nt * 8 + 2 * i + m) * 64 + lane) * 16);
+            // (staged in LDS by the tile's block 0: head_piece; landed and visible since that
+            // block's tap-8 wait and the barriers after it)
+            const uint4 hwf = *reinterpret_cast<const uint4*>(smem + OFF_HW + hsel * HWB + (2 * i + m) * 1024 + lane * 16);
             Mfma<T>::run(hwf, hv, hacc);
           }
           __builtin_amdgcn_sched_barrier(0);  // bound the live set: one 8-channel group at a time
@@ -613,6 +625,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // k-step index of the block's tap 0 within the tile body (a pair of tiles when NCB == 2)
     constexpr int P0 = decltype(tpos)::value * SPTK + CB * (9 + RES);
     step(IC<0>{}, IC<CB == 0>{}, IC<(P0 + 0) & 3>{});
+    // EPI 1: the tile's 1x1 head weights into LDS buffer tl & 1 (the other buffer may still be read
+    // by the previous tile's epilogue). Issued before this block's tap-5 halo piece, so the tap-8
+    // counted wait drains it; unconditional, like every main-loop VMEM operation.
+    if constexpr (EPI == 1 && CB == 0) head_piece(cur_nt, tl & 1);
     step(IC<1>{}, IC<false>{}, IC<(P0 + 1) & 3>{});
     step(IC<2>{}, IC<false>{}, IC<(P0 + 2) & 3>{});
     step(IC<3>{}, IC<false>{}, IC<(P0 + 3) & 3>{});
@@ -636,12 +652,12 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
   for (; tl < ntl;) {
     blocks(blocks, IC<0>{}, IC<0>{});
-    epilogue(cur_fr, cur_y0, cur_x0, cur_nt);
+    epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
     ++tl;
     if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
     if constexpr (UP == 2) {  // the pair's second unit (ntl is even)
       blocks(blocks, IC<0>{}, IC<1>{});
-      epilogue(cur_fr, cur_y0, cur_x0, cur_nt);
+      epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
       ++tl;
       if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
     }
@@ -651,7 +667,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4, int NCB = 4>
 inline int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
   auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>;
-  constexpr int lds = lds_bytes<RES>();
+  constexpr int lds = lds_bytes<RES, EPI>();
   if (int r = ensure_lds<conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>>(lds)) return r;
   hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, out);
   TV_HIP(hipGetLastError());

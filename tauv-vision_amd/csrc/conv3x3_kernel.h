@@ -69,8 +69,11 @@ constexpr int RPW = RBUF / 1024 / NW;           // residual pieces per wave per 
 // lanes x 16 B) staged by LDS-DMA into one of two buffers in the RES region, one 1 KiB piece per wave
 constexpr int OFF_HW = OFF_R;
 constexpr int HWB = 8 * 1024;
+// EPI 1: per wave a 32-pixel x 16-row fp32 scratch for the transposed head atomics
+constexpr int OFF_HS = OFF_HW + 2 * HWB;
+constexpr int HSW = 32 * 16 * 4;
 template <int RES, int EPI = 0>
-constexpr int lds_bytes() { return OFF_R + (RES ? RBUF : EPI ? 2 * HWB : 0); }
+constexpr int lds_bytes() { return OFF_R + (RES ? RBUF : EPI ? 2 * HWB + NW * HSW : 0); }
 static_assert(lds_bytes<1>() <= 160 * 1024 && lds_bytes<0, 1>() <= 160 * 1024, "LDS budget");
 static_assert(WSLOT / 1024 == NW, "one weight piece per wave per k-step");
 static_assert(HPIECES * 64 >= HPIX * 5, "halo pieces");
@@ -445,18 +448,37 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         }
       }
       if constexpr (EPI == 1) {
-        // rows r = 8G + 4lh + e of the 1x1 result: output column head_row0[nt] + r of pixel (y, x)
+        // rows r = 8G + 4lh + e of the 1x1 result (lane: pixel l32): output column head_row0[nt] + r
+        // of the pixel. The partial sums are added with float atomics (the two 128-channel halves
+        // of a 256-channel head meet in the output), which run at the memory side in 64-byte
+        // requests: a lane-per-pixel add touches 32 pixels' lines per instruction. So each half
+        // of 16 rows is transposed through this wave's LDS scratch first, and lane idx of the adds
+        // takes (pixel idx / n, row idx % n): one instruction covers 64 / n pixels' contiguous rows.
         const int nr = p.head_nrows[nt];
-        float* hd = reinterpret_cast<float*>(out_ptr) + ((size_t)(fr * H + (ok ? y : 0)) * W + (ok ? x : 0)) * p.head_ldc +
-                    p.head_row0[nt];
         const float* hb = p.head_b + nt * 32;
+        float* hs = reinterpret_cast<float*>(smem + OFF_HS + wave * HSW);
+        float* hout = reinterpret_cast<float*>(out_ptr) + p.head_row0[nt];
+        const int qf = WP * wave + 32 * f;  // the fragment's first pixel in the tile
 #pragma unroll
-        for (int G = 0; G < 4; ++G)
+        for (int hh = 0; hh < 2; ++hh) {
+          const int n = min(16, nr - 16 * hh);  // wave-uniform
+          if (n <= 0) break;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = 8 * G + 4 * lh + e;
-            if (ok && r < nr) unsafeAtomicAdd(hd + r, hacc[4 * G + e] + hb[r]);
+          for (int g = 0; g < 2; ++g) {
+            const int G = 2 * hh + g;
+            *reinterpret_cast<f32x4*>(hs + l32 * 16 + 8 * g + 4 * lh) =
+                f32x4{hacc[4 * G + 0], hacc[4 * G + 1], hacc[4 * G + 2], hacc[4 * G + 3]};
           }
+          // (this wave's own LDS writes and reads complete in issue order)
+          for (int idx = lane; idx < 32 * n; idx += 64) {
+            const int px = idx / n, r = idx - px * n;
+            const int qq = qf + px;
+            const int yy = y0 + qq / TW, xx = x0 + qq % TW;
+            if (yy < H && xx < W && fr < nframes)
+              unsafeAtomicAdd(hout + ((size_t)(fr * H + yy) * W + xx) * p.head_ldc + 16 * hh + r,
+                              hs[px * 16 + r] + hb[16 * hh + r]);
+          }
+        }
       }
     }
   };

@@ -178,6 +178,59 @@ __global__ __launch_bounds__(256) void dwconvt_add(const T* __restrict__ src, in
   }
 }
 
+// The same for the power-of-two upsampling factors of DLA-34 (f = 2, 4, 8) and a power-of-two
+// chunk count per pixel: shifts and masks instead of the signed divisions by f and the division by
+// the chunk count; the skip chunk is loaded before the taps. Same taps in the same order: identical
+// results.
+template <typename T, int LF>
+__global__ __launch_bounds__(256) void dwconvt_add_p2(const T* __restrict__ src, int B, int h, int w, int C,
+                                                      const float* __restrict__ weight, const T* __restrict__ add,
+                                                      int add_ldc, T* __restrict__ out, int tH, int tW, int sy, int sx,
+                                                      int lnq) {
+  constexpr int V = Vec<T>::N;
+  constexpr int f = 1 << LF, p = f / 2, k = 2 * f;
+  const unsigned total = ((unsigned)B * tH * tW) << lnq;
+  const unsigned i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const unsigned q = i & ((1u << lnq) - 1u);
+  const unsigned pix = i >> lnq;
+  const int x = (int)(pix % (unsigned)tW);
+  const unsigned r = pix / (unsigned)tW;
+  const int y = (int)(r % (unsigned)tH);
+  const unsigned b = r / (unsigned)tH;
+  Vec<T> s;
+  load_vec(add + (size_t)pix * add_ldc + q * V, s);
+  Vec<T> acc;
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc.v[e] = 0.f;
+  const int hu = (h - 1) * f - 2 * p + k, wu = (w - 1) * f - 2 * p + k;
+  const int u = y - sy, v = x - sx;
+  if (u >= 0 && u < hu && v >= 0 && v < wu) {
+    const int ky0 = (u + p) & (f - 1), kx0 = (v + p) & (f - 1);
+    const int iy0 = (u + p) >> LF, ix0 = (v + p) >> LF;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int iy = iy0 - a;
+      if (iy < 0 || iy >= h) continue;
+      const int ky = ky0 + a * f;
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        const int ix = ix0 - c2;
+        if (ix < 0 || ix >= w) continue;
+        const int kx = kx0 + c2 * f;
+        Vec<T> t;
+        load_vec(src + (((size_t)b * h + iy) * w + ix) * C + q * V, t);
+        const float* wp = weight + (ky * k + kx) * C + q * V;
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc.v[e] += t.v[e] * wp[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc.v[e] = acc.v[e] + s.v[e];
+  store_vec(out + (size_t)pix * C + q * V, acc);
+}
+
 inline int grid_for(long threads) { return (int)std::max<long>((threads + 255) / 256, 1); }
 
 }  // namespace dla
@@ -211,9 +264,17 @@ int dcn_t(const void* x, int B, int H, int W, int C, const void* om, int om_ldc,
 template <typename T>
 int dwconvt_t(const void* src, int B, int h, int w, int C, const float* weight, int f, const void* add, int add_ldc,
               void* out, int tH, int tW, int sy, int sx, hipStream_t s) {
-  const long n = (long)B * tH * tW * (C / dla::Vec<T>::N);
-  hipLaunchKernelGGL(dla::dwconvt_add<T>, dim3(dla::grid_for(n)), dim3(256), 0, s, (const T*)src, B, h, w, C, weight,
-                     f, (const T*)add, add_ldc, (T*)out, tH, tW, sy, sx);
+  const int nq = C / dla::Vec<T>::N;
+  const long n = (long)B * tH * tW * nq;
+  const int lnq = __builtin_ctz((unsigned)nq);
+  const int lf = (f == 2 || f == 4 || f == 8) && (nq & (nq - 1)) == 0 ? __builtin_ctz((unsigned)f) : 0;
+  auto kp = lf == 1 ? dla::dwconvt_add_p2<T, 1> : lf == 2 ? dla::dwconvt_add_p2<T, 2> : dla::dwconvt_add_p2<T, 3>;
+  if (lf)
+    hipLaunchKernelGGL(kp, dim3(dla::grid_for(n)), dim3(256), 0, s, (const T*)src, B, h, w, C, weight,
+                       (const T*)add, add_ldc, (T*)out, tH, tW, sy, sx, lnq);
+  else
+    hipLaunchKernelGGL(dla::dwconvt_add<T>, dim3(dla::grid_for(n)), dim3(256), 0, s, (const T*)src, B, h, w, C, weight,
+                       f, (const T*)add, add_ldc, (T*)out, tH, tW, sy, sx);
   TV_HIP(hipGetLastError());
   return 0;
 }

@@ -409,6 +409,11 @@ def run_yolact(args, world, rank, device):
     elapsed = timed(step, args.steps, args.warmup, world, device)
     value = world * B * args.steps / elapsed
     flops_frame = eng.geom["flops_per_frame"]
+    ranks = dist.get_world_size() if world > 1 else 1
+    if world > 1:
+        dist.destroy_process_group()  # the legs below are rank 0's alone (no collective)
+        if rank != 0:
+            return
 
     # dominant protonet kernel (per-launch HIP events) and the mask kernel's HBM rate
     prof = eng.profile(x, proto)
@@ -478,7 +483,7 @@ def run_yolact(args, world, rank, device):
                          f"oracle/ PyTorch-CPU restatement, bit-identical to the reference on CPU"}
     if rank == 0:
         line = {
-            "metric": YOLACT_METRIC, "value": round(value, 2), "unit": "frames/sec", "n_gpus": world,
+            "metric": YOLACT_METRIC, "value": round(value, 2), "unit": "frames/sec", "n_gpus": world, "ranks": ranks,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
             "data": "synthetic",
@@ -492,6 +497,68 @@ def run_yolact(args, world, rank, device):
             "detections_per_frame": round(kept / B, 2), "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+
+
+def launch_ranks(n):
+    """`--gpus N` (N > 1) run outside torch.distributed.run: start the N ranks as ONE child
+    `python -m torch.distributed.run` (rendezvous on 127.0.0.1) before this process touches
+    the GPU, and return its exit code (the parent never initialises HIP, so nothing is
+    exec'd over a GPU context)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
+def dryrun_records(frame, K):
+    """Deterministic stand-in for one frame's packed decode records (the --cpu-dryrun step)."""
+    r = torch.zeros((K, 10), dtype=torch.float32)
+    r[:, 0] = torch.arange(K) % N_LABELS
+    r[:, 1] = 1.0 - 0.001 * torch.arange(K) - 1e-6 * frame
+    r[:, 2:6] = frame + 0.25 * torch.arange(4)[None, :]
+    r[:, 7] = torch.arange(K) + 1000 * frame
+    return r, frame % (K + 1)
+
+
+def run_dryrun(args, world, rank):
+    """Launcher / sharding / gather plumbing check on CPU (gloo): every rank fills its
+    `batch` frames' records (global frames rank*B .. rank*B+B-1) and all-gathers them exactly
+    as the GPU step does (RecordGather); rank 0 checks the gathered block against the records
+    one process makes for all world*B frames. No kernels run: the line is not a measurement."""
+    B, K = args.batch, min(args.k, 8)
+    if world > 1:
+        dist.init_process_group("gloo")
+    rec = torch.zeros((B, K, 10))
+    cnt = torch.zeros((B,), dtype=torch.int32)
+    for i in range(B):
+        rec[i], cnt[i] = dryrun_records(rank * B + i, K)
+    gather = RecordGather(B, K, "cpu") if world > 1 else None
+    out = {}
+
+    def step():
+        out["rec"], out["cnt"] = gather(rec, cnt) if gather is not None else (rec, cnt)
+
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    el = time.perf_counter() - t0
+    if rank == 0:
+        want = [dryrun_records(f, K) for f in range(world * B)]
+        ok = all(torch.equal(out["rec"][f], want[f][0]) and int(out["cnt"][f]) == want[f][1]
+                 for f in range(world * B)) and out["rec"].shape[0] == world * B
+        print(json.dumps({"metric": "cpu-dryrun (launcher + frame sharding + record all-gather; no kernels)",
+                          "value": None, "unit": "frames/sec", "n_gpus": args.gpus,
+                          "ranks": dist.get_world_size() if world > 1 else 1,
+                          "backend": "gloo" if world > 1 else None, "batch_per_rank": B, "steps": args.steps,
+                          "gathered_frames": int(out["rec"].shape[0]), "gather_ok": bool(ok),
+                          "wall_s": round(el, 4)}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -516,6 +583,8 @@ def main():
     ap.add_argument("--b1-steps", type=int, default=200)
     ap.add_argument("--fp32-steps", type=int, default=3)
     ap.add_argument("--allow-env-knobs", action="store_true")
+    ap.add_argument("--cpu-dryrun", action="store_true",
+                    help="CPU/gloo check of the --gpus N launcher, frame sharding and record all-gather (no kernels)")
     ap.add_argument("--model", default="r18", choices=["r18", "dla34", "yolact"],
                     help="r18: the BASELINE CenterNet-R18 (headline); dla34: CenterpointDLA34, heads [4,4,8,2,2]; "
                          "yolact: protonet + post-processing at 550x550, batch 32 (BASELINE config 5)")
@@ -524,9 +593,17 @@ def main():
     if knobs and not args.allow_env_knobs:
         sys.exit(f"bench.py: TV_* environment knobs set ({knobs}); unset them or pass --allow-env-knobs")
 
+    if args.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))  # before any GPU call: the ranks are children
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_dryrun:
+        return run_dryrun(args, world, rank)
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
@@ -547,6 +624,12 @@ def main():
     elapsed = timed(lambda: pipe.step(frames, gather), args.steps, args.warmup, world, device)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
+    gathered = int(gather.rec.shape[0] * gather.rec.shape[1]) if gather is not None else B
+    ranks = dist.get_world_size() if world > 1 else 1
+    if world > 1:
+        dist.destroy_process_group()  # the legs below are rank 0's alone (no collective)
+        if rank != 0:
+            return
 
     # roofline of the dominant kernel (separate pass with per-launch events)
     roof = conv_roofline(pipe, frames, args.precision)
@@ -579,7 +662,8 @@ def main():
                     else "CenterpointDLA34 (DLA-34 + DLAUp/IDAUp with DCNv2, heads [4,4,8,2,2]) ")
         line = {
             "metric": METRIC if args.model == "r18" else METRIC.replace("CenterNet-R18", "CenterpointDLA34"),
-            "value": round(value, 2), "unit": "frames/sec", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 2), "unit": "frames/sec", "n_gpus": world, "ranks": ranks,
+            "gathered_frames_per_step": gathered, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"workload": workload + f"640x480 u8 frames, batch={B}/GPU, forward + decode(K={K}, thr={args.thr})",
@@ -593,8 +677,6 @@ def main():
         if knobs:
             line["env_knobs"] = knobs
         print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

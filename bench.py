@@ -567,6 +567,18 @@ def env_knobs():
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("TV_")}
 
 
+def forward_env_knobs(knobs):
+    """Diagnostics (A/B runs, tools/): hand TV_* knobs to the package explicitly — the library
+    and the package read no environment. TV_LIB = another build of the library."""
+    if not knobs:
+        return
+    from tauv_vision_amd import _lib
+    from tauv_vision_amd.engine import set_diagnostic_knobs
+    if "TV_LIB" in knobs:
+        _lib.set_library_path(knobs["TV_LIB"])
+    set_diagnostic_knobs({k: v for k, v in knobs.items() if k != "TV_LIB"})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -592,6 +604,7 @@ def main():
     knobs = env_knobs()
     if knobs and not args.allow_env_knobs:
         sys.exit(f"bench.py: TV_* environment knobs set ({knobs}); unset them or pass --allow-env-knobs")
+    forward_env_knobs(knobs)
 
     if args.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")

@@ -93,6 +93,12 @@ int tv_model_geometry(const tv_model_desc* desc, double* flops_per_frame, int32_
  * after create, so concurrent forwards on different streams are safe. */
 int tv_engine_create(const tv_model_desc* desc, const tv_weight_view* weights, int32_t n_weights,
                      int32_t device, tv_engine** out);
+/* Diagnostics only (kernel A/B experiments, tools/): tv_engine_create with kernel-choice
+ * overrides given explicitly as "NAME=VALUE;NAME=VALUE" (TV_C3_TW, TV_LAT, TV_SLICES, ... — the
+ * list in engine.cpp); an unknown name is TV_EINVAL. The product entry point above takes none
+ * and reads no environment variable. */
+int tv_engine_create_diag(const tv_model_desc* desc, const tv_weight_view* weights, int32_t n_weights,
+                          int32_t device, const char* knobs, tv_engine** out);
 int tv_engine_destroy(tv_engine* engine);
 /* Workspaces: the first forward of a batch size on a stream allocates that (stream, batch)
  * pair's activation arena (hipMalloc: not inside a graph capture) and keeps it for later calls;
@@ -208,6 +214,18 @@ int tv_yolact_assemble_masks_indexed(const float* mask_prototype, const int64_t 
                                      int32_t K, int32_t H, int32_t W, const float* mask_coeff, const float* box,
                                      int32_t A, const int64_t* det, const int32_t* counts, int32_t n_max, float* mask,
                                      void* stream);
+
+/* Diagnostics (GPU tests): one DeformConv2d(x, offset, sigmoid(mask)) (DeformConv.forward,
+ * centerpoint_dla.py:389-391: 3x3, stride 1, pad 1) + bias + activation (0 none, 1 ReLU, 2 leaky)
+ * through the kernel the engine uses for DLA-34's DeformConv layers. x: compute-dtype NHWC
+ * [B,H,W,C]; om: compute-dtype NHWC [B,H,W,om_ldc] = (dy, dx) per tap (18) + 9 mask logits (the
+ * engine's fused offset/mask conv output); weight: host fp32 [N][C][3][3], bias host fp32 [N];
+ * out: compute-dtype NHWC [B,H,W,N]. variant: 0 = fused dcn_gemm (32-channel k-steps),
+ * 1 = fused dcn_gemm64 (tile by size), 2 = dcn_gemm64 with 64-pixel tiles, 3 = unfused sampling +
+ * implicit GEMM (the fp32 path; the only variant for TV_F32). Synchronous; allocates. */
+int tv_diag_dcn_conv(const void* x, const void* om, int32_t B, int32_t H, int32_t W, int32_t C, int32_t om_ldc,
+                     const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, int32_t variant,
+                     void* out, void* stream);
 
 const char* tv_last_error(void);
 const char* tv_version(void);

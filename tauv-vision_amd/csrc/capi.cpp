@@ -91,6 +91,32 @@ int tv_engine_create(const tv_model_desc* d, const tv_weight_view* w, int32_t n,
   })
 }
 
+int tv_engine_create_diag(const tv_model_desc* d, const tv_weight_view* w, int32_t n, int32_t device,
+                          const char* knobs, tv_engine** out) {
+  TV_GUARD({
+    if (!d || !out || (n && !w)) { set_error("null argument"); return TV_EINVAL; }
+    std::vector<std::pair<std::string, std::string>> kv;
+    for (const char* c = knobs ? knobs : ""; *c;) {
+      const char* e = c;
+      while (*e && *e != ';') ++e;
+      std::string item(c, e);
+      c = *e ? e + 1 : e;
+      if (item.empty()) continue;
+      const size_t eq = item.find('=');
+      if (eq == std::string::npos) { set_error("engine knob without '=': " + item); return TV_EINVAL; }
+      kv.emplace_back(item.substr(0, eq), item.substr(eq + 1));
+    }
+    tv_engine* e = new tv_engine();
+    int rc = e->e.create(*d, w, n, device, kv);
+    if (rc) {
+      delete e;
+      return rc;
+    }
+    *out = e;
+    return TV_OK;
+  })
+}
+
 int tv_engine_destroy(tv_engine* e) {
   TV_GUARD({
     delete e;
@@ -338,6 +364,13 @@ int tv_decode(const float* heat, const int64_t hs[4], const float* size, const i
     p.counts = counts;
     return launch_decode(heat, hs, B, C, H, W, K, ws, (size_t)ws_bytes, p, s);
   })
+}
+
+int tv_diag_dcn_conv(const void* x, const void* om, int32_t B, int32_t H, int32_t W, int32_t C, int32_t om_ldc,
+                     const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, int32_t variant,
+                     void* out, void* stream) {
+  TV_GUARD({ return tv::diag_dcn_conv(x, om, B, H, W, C, om_ldc, weight, bias, N, act, dtype, variant, out,
+                                      (hipStream_t)stream); })
 }
 
 }  // extern "C"

@@ -146,6 +146,9 @@ struct DcnParams {
 };
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad);
 int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, hipStream_t s);  // dcn64_mode: 64-channel k-steps when C % 64 == 0
+// diag.cpp: one DeformConv2d + bias + activation through a chosen DCN kernel (GPU tests)
+int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int om_ldc, const float* weight,
+                  const float* bias, int N, int act, int dtype, int variant, void* out, hipStream_t s);
 
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
 // output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC

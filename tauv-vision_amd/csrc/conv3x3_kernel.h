@@ -432,17 +432,30 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
             raw_buffer_store_v4(u32x4{r0[0], r1[0], r0[1], r1[1]}, orsrc,
                                 ch < p.N ? (int)(obase + (unsigned)((32 * i + 16 * m) * sizeof(OutT))) : (int)0x80000000u, 0, 0);
           } else {
-            // the 8 hidden channels 32i+16m+8lh.. of this pixel, rounded to T exactly as the
-            // unfused path stores them, are the MFMA B operand of k-step 2i+m of the 1x1
+            // the 8 hidden channels 32i+16m+8lh.. of this pixel are the MFMA B operand of k-step
+            // 2i+m of the 1x1, as a hi + lo pair of T values (hi = T(v), lo = T(v - hi)): the
+            // 1x1 sees the fp32 hidden activation to ~2x T's precision, not its T rounding
+            // (the reference's hidden tensor is fp32; +16 MFMAs per 576-MFMA tile)
+            float lo[2][4];
+#pragma unroll
+            for (int gg = 0; gg < 2; ++gg)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) lo[gg][e] = v[gg][e] - (float)(T)v[gg][e];
             const unsigned a0 = pack2<T>(v[0][0], v[0][1]), a1 = pack2<T>(v[0][2], v[0][3]);
             const unsigned b0 = pack2<T>(v[1][0], v[1][1]), b1 = pack2<T>(v[1][2], v[1][3]);
             const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
             const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
             const uint4 hv = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+            const unsigned c0 = pack2<T>(lo[0][0], lo[0][1]), c1 = pack2<T>(lo[0][2], lo[0][3]);
+            const unsigned d0 = pack2<T>(lo[1][0], lo[1][1]), d1 = pack2<T>(lo[1][2], lo[1][3]);
+            const auto s0 = __builtin_amdgcn_permlane32_swap(c0, d0, false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(c1, d1, false, false);
+            const uint4 hl = make_uint4(s0[0], s1[0], s0[1], s1[1]);
             // (staged in LDS by the tile's block 0: head_piece; landed and visible since that
             // block's tap-8 wait and the barriers after it)
             const uint4 hwf = *reinterpret_cast<const uint4*>(smem + OFF_HW + hsel * HWB + (2 * i + m) * 1024 + lane * 16);
             Mfma<T>::run(hwf, hv, hacc);
+            Mfma<T>::run(hwf, hl, hacc);
           }
           __builtin_amdgcn_sched_barrier(0);  // bound the live set: one 8-channel group at a time
         }
@@ -469,7 +482,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
             *reinterpret_cast<f32x4*>(hs + l32 * 16 + 8 * g + 4 * lh) =
                 f32x4{hacc[4 * G + 0], hacc[4 * G + 1], hacc[4 * G + 2], hacc[4 * G + 3]};
           }
-          // (this wave's own LDS writes and reads complete in issue order)
+          // lanes read rows other lanes wrote: order the wave's LDS writes before its reads
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
           for (int idx = lane; idx < 32 * n; idx += 64) {
             const int px = idx / n, r = idx - px * n;
             const int qq = qf + px;
@@ -478,6 +494,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
               unsafeAtomicAdd(hout + ((size_t)(fr * H + yy) * W + xx) * p.head_ldc + 16 * hh + r,
                               hs[px * 16 + r] + hb[16 * hh + r]);
           }
+          // ... and those reads before the next half's / fragment's writes of the scratch
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
       }
     }

@@ -277,8 +277,15 @@ template <int BN> constexpr int wbuf2() { return BN * ROW2; }
 template <int PX> constexpr int pslot() { return PX * 32; }  // one tap's sampling state: (4 int + 4 float) per pixel
 template <int BN, int PX> constexpr int lds_bytes2() { return 2 * (abuf2<PX>() + wbuf2<BN>()) + 3 * pslot<PX>(); }
 
+// resident workgroups per CU the register budget is sized for: as many as the LDS admits (<= 4)
+template <int BN, int PX> constexpr int min_blocks2() {
+  return 160 * 1024 / lds_bytes2<BN, PX>() < 4 ? 160 * 1024 / lds_bytes2<BN, PX>() : 4;
+}
+static_assert(min_blocks2<64, 64>() == 4 && min_blocks2<128, 64>() == 2 && min_blocks2<128, 128>() == 2,
+              "dcn_gemm64 occupancy hints follow the LDS budget");
+
 template <typename T, int BN, int PX>
-__global__ __launch_bounds__(NT, PX == 64 ? (BN == 64 ? 4 : 3) : 2) void dcn_gemm64(const DcnParams p) {
+__global__ __launch_bounds__(NT, (min_blocks2<BN, PX>())) void dcn_gemm64(const DcnParams p) {
   constexpr int PJ = PX / 32;            // pixels per thread per k-step
   constexpr int WPX = PX / 32;           // waves along pixels (32 each); the rest split the channels
   constexpr int NA = BN / 32 / (4 / WPX);  // 32-channel accumulator blocks per wave

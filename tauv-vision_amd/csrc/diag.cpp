@@ -1,0 +1,134 @@
+// Diagnostic C-ABI entry points (include/tauv_vision_amd.h, "Diagnostics"): single kernels driven
+// directly, for the GPU tests that pin them to identities the reference implies. Not on the
+// product path (synchronous, allocate per call).
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "../../include/tauv_vision_amd.h"
+
+namespace {
+
+uint16_t to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7F800000u) == 0x7F800000u && (u & 0x7FFFFFu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+void put(std::vector<uint8_t>& buf, size_t i, float v, int dtype) {
+  if (dtype == tv::F32) {
+    std::memcpy(buf.data() + 4 * i, &v, 4);
+  } else if (dtype == tv::F16) {
+    const _Float16 h = (_Float16)v;
+    std::memcpy(buf.data() + 2 * i, &h, 2);
+  } else {
+    const uint16_t b = to_bf16(v);
+    std::memcpy(buf.data() + 2 * i, &b, 2);
+  }
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+}  // namespace
+
+namespace tv {
+
+// DeformConv2d(x, offset, sigmoid(mask)) (torchvision semantics as used by DeformConv.forward,
+// centerpoint_dla.py:389-391; 3x3, stride 1, pad 1) + bias + activation, as the engine runs it:
+// variant 0 = fused dcn_gemm (32-channel k-steps), 1 = fused dcn_gemm64 (tile by size),
+// 2 = dcn_gemm64 with 64-pixel tiles, 3 = unfused (dcn_sample column tensor + implicit GEMM: the
+// fp32 path). weight: host fp32 [N][C][3][3] (PyTorch layout), K packed tap-major as the engine does.
+int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int om_ldc, const float* weight,
+                  const float* bias, int N, int act, int dtype, int variant, void* out, hipStream_t s) {
+  if (!x || !om || !weight || !bias || !out || B < 1 || H < 1 || W < 1 || C < 1 || N < 1 || om_ldc < 27 ||
+      variant < 0 || variant > 3 || dtype < F32 || dtype > BF16 || act < 0 || act > 2) {
+    set_error("diag_dcn_conv: bad argument");
+    return TV_EINVAL;
+  }
+  if (dtype == F32 && variant != 3) {
+    set_error("diag_dcn_conv: the fused kernels are fp16/bf16 (fp32 runs variant 3)");
+    return TV_EINVAL;
+  }
+  const int esz = dtype_size(dtype);
+  const int BK = 128 / esz;  // one 128-byte k-step
+  const int K = 9 * C;
+  const int ksteps = (K + BK - 1) / BK;
+  const int Kpad = ksteps * BK;
+  const int Npad = (N + 127) / 128 * 128;
+  std::vector<uint8_t> hw((size_t)Npad * Kpad * esz, 0);
+  for (int n = 0; n < N; ++n)
+    for (int c = 0; c < C; ++c)
+      for (int t = 0; t < 9; ++t) put(hw, (size_t)n * Kpad + (size_t)t * C + c, weight[((size_t)n * C + c) * 9 + t], dtype);
+  std::vector<float> hb(Npad, 0.f);
+  std::memcpy(hb.data(), bias, N * sizeof(float));
+  DevBuf dw, db, dcols, dpar, dzero;
+  TV_HIP(hipMalloc(&dw.p, hw.size()));
+  TV_HIP(hipMemcpy(dw.p, hw.data(), hw.size(), hipMemcpyHostToDevice));
+  TV_HIP(hipMalloc(&db.p, hb.size() * 4));
+  TV_HIP(hipMemcpy(db.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  int rc = 0;
+  if (variant < 3) {
+    DcnParams q{};
+    q.x = x;
+    q.B = B;
+    q.H = H;
+    q.W = W;
+    q.C = C;
+    q.ldx = C;
+    q.om = om;
+    q.om_ldc = om_ldc;
+    q.w = dw.p;
+    q.Kpad = Kpad;
+    q.bias = (const float*)db.p;
+    q.act = act;
+    q.out = out;
+    q.out_ldc = N;
+    q.N = N;
+    if (variant >= 1 && C % 64) {
+      set_error("diag_dcn_conv: dcn_gemm64 needs C % 64 == 0");
+      return TV_EINVAL;
+    }
+    rc = launch_dcn_gemm(q, dtype, variant, s);
+  } else {
+    const size_t cols_bytes = (size_t)B * H * W * K * esz;
+    TV_HIP(hipMalloc(&dcols.p, cols_bytes));
+    TV_HIP(hipMalloc(&dzero.p, 256));
+    TV_HIP(hipMemset(dzero.p, 0, 256));
+    rc = launch_dcn_sample(x, B, H, W, C, om, om_ldc, dcols.p, dtype, s);
+    if (!rc) {
+      ConvParams p{};
+      p.seg[0] = ConvSegment{dcols.p, H, W, K, K, 1, 1, 1, 0, 0, ksteps, 0};
+      p.nseg = 1;
+      p.Ho = H;
+      p.Wo = W;
+      p.M = B * H * W;
+      p.N = N;
+      p.Kpad = Kpad;
+      p.weight = dw.p;
+      p.bias = (const float*)db.p;
+      p.act = act;
+      p.out = out;
+      p.out_ldc = N;
+      p.mtiles = (p.M + 127) / 128;
+      p.ntiles = Npad / 128;
+      p.zero = dzero.p;
+      TV_HIP(hipMalloc(&dpar.p, sizeof(ConvParams)));
+      TV_HIP(hipMemcpy(dpar.p, &p, sizeof(ConvParams), hipMemcpyHostToDevice));
+      rc = launch_conv(p, (const ConvParams*)dpar.p, out, dtype, 0, 0, s);
+    }
+  }
+  if (rc) return rc == TV_EHIP ? rc : TV_EINVAL;
+  TV_HIP(hipStreamSynchronize(s));  // the staging buffers are freed on return
+  return TV_OK;
+}
+
+}  // namespace tv

@@ -270,7 +270,8 @@ int Engine::pack_op(size_t oi) {
   return TV_OK;
 }
 
-int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev) {
+int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev,
+                   const std::vector<std::pair<std::string, std::string>>& knobs) {
   desc = d;
   device = dev;
   dtype = d.compute_dtype;
@@ -286,32 +287,42 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
   TV_HIP(hipSetDevice(device));
   TV_HIP(hipMalloc(&zero_page, 256));
   TV_HIP(hipMemset(zero_page, 0, 256));
-  if (const char* env = std::getenv("TV_CONV_PIPE")) pipe_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_CONV3")) conv3_mode = std::atoi(env);
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
       cu_count = ncu;
   }
-  if (const char* env = std::getenv("TV_C3_TW")) c3_tw_force = std::atoi(env) == 16 ? 16 : std::atoi(env) == 32 ? 32 : 0;
-  if (const char* env = std::getenv("TV_CUS")) cu_count = std::max(8, std::min(cu_count, std::atoi(env)));
-  if (const char* env = std::getenv("TV_STEM")) stem_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_LAT")) lat_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_LAT_UNITS")) lat_units = std::atoi(env);
-  if (const char* env = std::getenv("TV_DCN64")) dcn64_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_CONVT")) convt_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_CONV3S2")) s2_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_CONV3_MINPIX")) conv3_min_pix = std::atoi(env);
-  if (const char* env = std::getenv("TV_HEADFUSE")) headfuse_mode = std::atoi(env);
-  if (const char* env = std::getenv("TV_S2_MINTILES")) s2_min_tiles = std::atoi(env);
-  if (const char* env = std::getenv("TV_C3_NI")) c3_ni_force = std::atoi(env) == 2 ? 2 : std::atoi(env) == 4 ? 4 : 0;
-  if (const char* env = std::getenv("TV_C3_HALF_COST")) c3_half_cost = std::atoi(env);
-  if (const char* env = std::getenv("TV_SLICES")) slices = std::max(1, std::min(kMaxSlices, std::atoi(env)));
-  if (const char* env = std::getenv("TV_SLICE_SIZES")) {
-    for (const char* c = env; *c;) {
-      slice_sizes_env.push_back(std::atoi(c));
-      while (*c && *c != ',') ++c;
-      if (*c == ',') ++c;
+  // diagnostics only (tv_engine_create_diag): kernel-choice overrides for A/B experiments; the
+  // product entry point (tv_engine_create) passes none and reads no environment
+  for (const auto& kv : knobs) {
+    const std::string& k = kv.first;
+    const char* env = kv.second.c_str();
+    const int v = std::atoi(env);
+    if (k == "TV_CONV_PIPE") pipe_mode = v;
+    else if (k == "TV_CONV3") conv3_mode = v;
+    else if (k == "TV_C3_TW") c3_tw_force = v == 16 ? 16 : v == 32 ? 32 : 0;
+    else if (k == "TV_CUS") cu_count = std::max(8, std::min(cu_count, v));
+    else if (k == "TV_STEM") stem_mode = v;
+    else if (k == "TV_LAT") lat_mode = v;
+    else if (k == "TV_LAT_UNITS") lat_units = v;
+    else if (k == "TV_DCN64") dcn64_mode = v;
+    else if (k == "TV_CONVT") convt_mode = v;
+    else if (k == "TV_CONV3S2") s2_mode = v;
+    else if (k == "TV_CONV3_MINPIX") conv3_min_pix = v;
+    else if (k == "TV_HEADFUSE") headfuse_mode = v;
+    else if (k == "TV_S2_MINTILES") s2_min_tiles = v;
+    else if (k == "TV_C3_NI") c3_ni_force = v == 2 ? 2 : v == 4 ? 4 : 0;
+    else if (k == "TV_C3_HALF_COST") c3_half_cost = v;
+    else if (k == "TV_SLICES") slices = std::max(1, std::min(kMaxSlices, v));
+    else if (k == "TV_SLICE_SIZES") {
+      for (const char* c = env; *c;) {
+        slice_sizes_env.push_back(std::atoi(c));
+        while (*c && *c != ',') ++c;
+        if (*c == ',') ++c;
+      }
+    } else {
+      set_error("unknown engine knob: " + k);
+      return TV_EINVAL;
     }
   }
   // fused staging + stem (stem.hip): the row-expanded 7x7 conv right after the staging op
@@ -375,6 +386,23 @@ int Engine::make_workspace(int B, Workspace* ws) {
       last[plan.ops[i - 1].add] = std::max(last[plan.ops[i - 1].add], (int)i);
     }
   }
+  // DCNv2 sampling + its column GEMM that run as one fused kernel (dcn.hip): the column tensor
+  // (B x H x W x 9C) is never materialised, so it gets no arena space
+  auto dcn_fusable = [&](size_t i) {
+    if (dtype == F32 || i + 1 >= plan.ops.size()) return false;
+    const OpSpec& d = plan.ops[i];
+    const OpSpec& g = plan.ops[i + 1];
+    if (d.kind != OP_DCN || g.kind != OP_CONV || g.segs.size() != 1 || g.segs[0].src != d.out ||
+        g.segs[0].row_expand != 9 || g.out < 0 || g.add >= 0)
+      return false;
+    const TensorSpec& xt = plan.tensors[d.src];
+    return dcn_gemm_supported((long)B * xt.H * xt.W, xt.C, g.N, xt.C, plan.tensors[d.add].C, plan.tensors[g.out].C,
+                              packed[i + 1].Kpad) &&
+           g.segs[0].cin == xt.C;
+  };
+  std::vector<char> virt(nt, 0);
+  for (size_t i = 0; i < plan.ops.size(); ++i)
+    if (dcn_fusable(i)) virt[plan.ops[i].out] = 1;
   ws->off.assign(nt, 0);
   struct Live { size_t off, size; int last; };
   std::vector<Live> live;
@@ -384,6 +412,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
     const OpSpec& op = plan.ops[i];
     live.erase(std::remove_if(live.begin(), live.end(), [&](const Live& l) { return l.last < (int)i; }), live.end());
     if (op.out < 0 || (stem_op >= 0 && op.kind == OP_PREP)) continue;  // fused stem: no staged input
+    if (virt[op.out]) continue;                                          // fused DCN: no column tensor
     if (placed[op.out]) continue;
     placed[op.out] = 1;
     const TensorSpec& t = plan.tensors[op.out];
@@ -626,18 +655,13 @@ int Engine::make_workspace(int B, Workspace* ws) {
   // DCNv2 sampling + its column GEMM -> one fused kernel (dcn.hip)
   ws->dcn_skip.assign(plan.ops.size(), 0);
   ws->dcn.assign(plan.ops.size(), DcnParams{});
-  for (size_t i = 0; dtype != F32 && i + 1 < plan.ops.size(); ++i) {
+  for (size_t i = 0; i + 1 < plan.ops.size(); ++i) {
+    if (!dcn_fusable(i)) continue;
     const OpSpec& d = plan.ops[i];
     const OpSpec& g = plan.ops[i + 1];
-    if (d.kind != OP_DCN || g.kind != OP_CONV || g.segs.size() != 1 || g.segs[0].src != d.out ||
-        g.segs[0].row_expand != 9 || g.out < 0 || g.add >= 0)
-      continue;
     const TensorSpec& xt = plan.tensors[d.src];
     const TensorSpec& omt = plan.tensors[d.add];
     const TensorSpec& ot = plan.tensors[g.out];
-    if (!dcn_gemm_supported((long)B * xt.H * xt.W, xt.C, g.N, xt.C, omt.C, ot.C, packed[i + 1].Kpad) ||
-        g.segs[0].cin != xt.C)
-      continue;
     DcnParams& q = ws->dcn[i + 1];
     q.x = base + ws->off[d.src];
     q.B = B;

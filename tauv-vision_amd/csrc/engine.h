@@ -80,7 +80,7 @@ struct Engine {
   // concurrent slices: a batch of >= slices * slice_min frames runs as `slices` near-equal parts,
   // the first on the caller's stream and the others on side streams (fork / join events), so one
   // slice's latency-bound small layers and grid tails overlap another's large layers
-  // (env TV_SLICES: count, 1 = off; TV_SLICE_SIZES=a,b,...: explicit sizes for experiments)
+  // (knob TV_SLICES: count, 1 = off; TV_SLICE_SIZES=a,b,...: explicit sizes for experiments)
   static constexpr int kMaxSlices = 8;  // == TV_MAX_SLICES (include/tauv_vision_amd.h)
   int slices = 2;
   int slice_min = 8;
@@ -97,7 +97,8 @@ struct Engine {
   std::unordered_map<std::string, std::pair<const float*, int64_t>> host_w;  // during create only
 
   ~Engine();
-  int create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev);
+  int create(const tv_model_desc& d, const tv_weight_view* w, int n, int dev,
+             const std::vector<std::pair<std::string, std::string>>& knobs = {});
   int get_workspace(int B, hipStream_t s, Workspace** out);
   int prepare(int B, hipStream_t s);  // workspaces (and side stream) for forward(B) on s
   int trim();                         // free every cached workspace (no forward may be in flight)

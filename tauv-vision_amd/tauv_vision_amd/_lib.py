@@ -8,8 +8,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# TV_LIB: load an alternative build of the library (kernel A/B experiments)
-LIB_PATH = os.environ.get("TV_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libtauv_vision_amd.so")
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtauv_vision_amd.so")
 
 TV_OK, TV_EINVAL, TV_ESHAPE, TV_EHIP, TV_ENOTFOUND, TV_ENOMEM = range(6)
 DTYPES = {"fp32": 0, "fp16": 1, "bf16": 2}
@@ -35,6 +34,8 @@ EXPORTS = {
                            ctypes.POINTER(c_i32), ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)], c_i32),
     "tv_engine_create": ([ctypes.POINTER(ModelDesc), ctypes.POINTER(WeightView), c_i32, c_i32,
                           ctypes.POINTER(c_vp)], c_i32),
+    "tv_engine_create_diag": ([ctypes.POINTER(ModelDesc), ctypes.POINTER(WeightView), c_i32, c_i32,
+                               ctypes.c_char_p, ctypes.POINTER(c_vp)], c_i32),
     "tv_engine_destroy": ([c_vp], c_i32),
     "tv_engine_prepare": ([c_vp, c_i32, c_vp], c_i32),
     "tv_engine_trim": ([c_vp], c_i32),
@@ -67,12 +68,23 @@ EXPORTS = {
                                   c_vp, c_vp], c_i32),
     "tv_yolact_assemble_masks_indexed": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32,
                                           c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
+    "tv_diag_dcn_conv": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
+                          c_vp, c_vp], c_i32),
     "tv_last_error": ([], ctypes.c_char_p),
     "tv_version": ([], ctypes.c_char_p),
 }
 
 _lib = None
 _lock = threading.Lock()
+
+
+def set_library_path(path):
+    """Diagnostics only (kernel A/B experiments): load another build of the library. Must be
+    called before the first call into the library; the package reads no environment."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("tauv_vision_amd: the HIP library is already loaded")
+    LIB_PATH = path
 
 
 def lib():

@@ -8,6 +8,17 @@ from . import _lib
 from .weights import geometry
 
 
+_DIAG_KNOBS = {}
+
+
+def set_diagnostic_knobs(knobs):
+    """Diagnostics only (kernel A/B experiments): kernel-choice overrides ({"TV_C3_TW": "16", ...},
+    the names engine.cpp lists) for engines created after this call, through
+    tv_engine_create_diag. The product path passes none and reads no environment."""
+    global _DIAG_KNOBS
+    _DIAG_KNOBS = {str(k): str(v) for k, v in (knobs or {}).items()}
+
+
 class NativeEngine:
     def __init__(self, desc, state_dict, device_index):
         self.desc = desc
@@ -26,8 +37,13 @@ class NativeEngine:
         handle = ctypes.c_void_p()
         L = _lib.lib()
         with torch.cuda.device(self.device):
-            _lib.check(L.tv_engine_create(ctypes.byref(desc), views, len(host), device_index, ctypes.byref(handle)),
-                       "engine create")
+            if _DIAG_KNOBS:
+                spec = ";".join(f"{k}={v}" for k, v in sorted(_DIAG_KNOBS.items())).encode()
+                rc = L.tv_engine_create_diag(ctypes.byref(desc), views, len(host), device_index, spec,
+                                             ctypes.byref(handle))
+            else:
+                rc = L.tv_engine_create(ctypes.byref(desc), views, len(host), device_index, ctypes.byref(handle))
+            _lib.check(rc, "engine create")
         self._h = handle
         del keep, host
 

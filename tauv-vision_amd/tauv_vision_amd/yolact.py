@@ -219,29 +219,48 @@ def assemble_mask(mask_prototype: torch.Tensor, mask_coeff: torch.Tensor,
     return out
 
 
+def _check_out(out, shape, device, what):
+    """A caller-supplied output: the kernel writes [B, n, H, W] fp32 through its raw pointer."""
+    if out is None:
+        return torch.empty(shape, dtype=torch.float32, device=device)
+    if tuple(out.shape) != tuple(shape) or out.dtype != torch.float32 or not out.is_contiguous() \
+            or out.device != device:
+        raise ValueError(f"{what}: out must be a contiguous fp32 {list(shape)} tensor on {device}, got "
+                         f"{out.dtype} {list(out.shape)} on {out.device}")
+    return out
+
+
+def _on(t, device, what):
+    if t.device != device:
+        raise ValueError(f"{what} is on {t.device}, the prototypes on {device}")
+    return t
+
+
 def assemble_masks(mask_prototype: torch.Tensor, mask_coeff: torch.Tensor, box: Optional[torch.Tensor],
                    counts: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """assemble_mask for B images: prototypes [B, K, H, W] (any strides), coefficients
     [B, n, K], boxes [B, n, 4] or None, counts [B] int32 on the device (detections per image;
     None = all n) -> masks [B, n, H, W] (rows past counts[b] are left untouched)."""
     proto = _proto_view(mask_prototype, "mask_prototype")
-    coeff = _f32(mask_coeff, "mask_coeff")
+    coeff = _on(_f32(mask_coeff, "mask_coeff"), proto.device, "mask_coeff")
+    if proto.dim() != 4 or coeff.dim() != 3:
+        raise ValueError(f"assemble_masks: prototypes {tuple(proto.shape)} / coefficients {tuple(coeff.shape)}")
     B, K, H, W = proto.shape
     n = coeff.shape[1]
     if coeff.shape != (B, n, K):
         raise ValueError(f"assemble_masks: coefficients {tuple(coeff.shape)} must be [{B}, n, {K}]")
     bptr = cptr = None
     if box is not None:
-        box = _f32(box, "box")
+        box = _on(_f32(box, "box"), proto.device, "box")
         if box.shape != (B, n, 4):
             raise ValueError(f"assemble_masks: box {tuple(box.shape)} must be [{B}, {n}, 4]")
         bptr = ctypes.c_void_p(box.data_ptr())
     if counts is not None:
-        if counts.dtype != torch.int32 or counts.shape != (B,) or not counts.is_cuda:
-            raise ValueError("assemble_masks: counts must be a device int32 [B] tensor")
+        if counts.dtype != torch.int32 or counts.shape != (B,) or counts.device != proto.device \
+                or not counts.is_contiguous():
+            raise ValueError("assemble_masks: counts must be a contiguous int32 [B] tensor on the prototypes' device")
         cptr = ctypes.c_void_p(counts.data_ptr())
-    if out is None:
-        out = torch.empty((B, n, H, W), dtype=torch.float32, device=proto.device)
+    out = _check_out(out, (B, n, H, W), proto.device, "assemble_masks")
     _lib.check(_lib.lib().tv_yolact_assemble_masks(ctypes.c_void_p(proto.data_ptr()), _lib.strides(proto, 4), B, K, H, W,
                                                    ctypes.c_void_p(coeff.data_ptr()), bptr, cptr, n,
                                                    ctypes.c_void_p(out.data_ptr()), _lib.stream_of(proto.device)),
@@ -256,7 +275,13 @@ def assemble_masks_indexed(mask_prototype: torch.Tensor, mask_coeff: torch.Tenso
     det [B, n] int64 / counts [B] int32 (BatchedNMS outputs) -> masks [B, n, H, W]; rows past
     counts[b] are left untouched."""
     proto = _proto_view(mask_prototype, "mask_prototype")
-    coeff = _f32(mask_coeff, "mask_coeff")
+    coeff = _on(_f32(mask_coeff, "mask_coeff"), proto.device, "mask_coeff")
+    if proto.dim() != 4 or coeff.dim() != 3 or det.dim() != 2:
+        raise ValueError("assemble_masks_indexed: need prototypes [B, K, H, W], coeff [B, A, K], det [B, n]")
+    _on(det, proto.device, "det")
+    _on(counts, proto.device, "counts")
+    if not det.is_contiguous() or not counts.is_contiguous():
+        raise ValueError("assemble_masks_indexed: det and counts must be contiguous")
     B, K, H, W = proto.shape
     A = coeff.shape[1]
     n = det.shape[1]
@@ -265,12 +290,11 @@ def assemble_masks_indexed(mask_prototype: torch.Tensor, mask_coeff: torch.Tenso
         raise ValueError("assemble_masks_indexed: need coeff [B, A, K], det [B, n] int64, counts [B] int32")
     bptr = None
     if box is not None:
-        box = _f32(box, "box")
+        box = _on(_f32(box, "box"), proto.device, "box")
         if box.shape != (B, A, 4):
             raise ValueError(f"assemble_masks_indexed: box {tuple(box.shape)} must be [{B}, {A}, 4]")
         bptr = ctypes.c_void_p(box.data_ptr())
-    if out is None:
-        out = torch.empty((B, n, H, W), dtype=torch.float32, device=proto.device)
+    out = _check_out(out, (B, n, H, W), proto.device, "assemble_masks_indexed")
     _lib.check(_lib.lib().tv_yolact_assemble_masks_indexed(
         ctypes.c_void_p(proto.data_ptr()), _lib.strides(proto, 4), B, K, H, W, ctypes.c_void_p(coeff.data_ptr()), bptr,
         A, ctypes.c_void_p(det.data_ptr()), ctypes.c_void_p(counts.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),

@@ -3,7 +3,7 @@ workgroup) against the reference goldens.
 
 By default the engine picks conv_lat only for layers its other kernels spread over fewer work
 units than there are CUs (the deep DLA levels). These tests force it onto every eligible layer
-(TV_LAT_UNITS huge) at B = 1 and 3, so 3x3 / stride-2 / Root concatenations / the
+(diagnostic knob TV_LAT_UNITS huge) at B = 1 and 3, so 3x3 / stride-2 / Root concatenations / the
 fused 1x1 residual / DLA-34's identity residuals all run through it at full size, and compare
 with the reference outputs at the same tolerances as the default path (test_gpu_forward.py,
 test_gpu_dla34.py).
@@ -20,7 +20,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _force(monkeypatch):
-    monkeypatch.setenv("TV_LAT_UNITS", str(10 ** 9))
+    """Engines built in this test get the diagnostic knob TV_LAT_UNITS (tv_engine_create_diag);
+    the product path reads no environment."""
+    from tauv_vision_amd import engine as E
+    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_LAT_UNITS": str(10 ** 9)})
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])

@@ -217,6 +217,31 @@ def test_gpu_assemble_masks_batched():
         assert (out[b, c:] == -1.0).all()  # rows past the count untouched
 
 
+@pytest.mark.gpu
+def test_gpu_assemble_masks_rejects_bad_out():
+    """A caller-supplied `out` / index tensor reaches the kernel as a raw pointer: wrong shape,
+    dtype, layout or device is refused before any launch (nothing is written)."""
+    from tauv_vision_amd.yolact import assemble_masks, assemble_masks_indexed
+    B, K, H, W, n, A = 2, 8, 9, 13, 3, 20
+    proto = torch.randn(B, K, H, W).cuda()
+    coeff = torch.randn(B, n, K).cuda()
+    for bad in (torch.empty(B, n, H, W + 1).cuda(), torch.empty(B, n, H, W, dtype=torch.float16).cuda(),
+                torch.empty(B, n, W, H).cuda().transpose(2, 3), torch.empty(B, n, H, W)):
+        with pytest.raises(ValueError):
+            assemble_masks(proto, coeff, None, out=bad)
+    with pytest.raises(ValueError):
+        assemble_masks(proto, coeff, None, counts=torch.zeros(B, dtype=torch.int32))  # host counts
+    acoeff = torch.randn(B, A, K).cuda()
+    det = torch.zeros(B, n, dtype=torch.int64).cuda()
+    cnt = torch.ones(B, dtype=torch.int32).cuda()
+    with pytest.raises(ValueError):
+        assemble_masks_indexed(proto, acoeff, None, det.cpu(), cnt)
+    with pytest.raises(ValueError):
+        assemble_masks_indexed(proto, acoeff, None, det, cnt, out=torch.empty(B, n + 1, H, W).cuda())
+    good = assemble_masks_indexed(proto, acoeff, None, det, cnt, out=torch.empty(B, n, H, W).cuda())
+    assert good.shape == (B, n, H, W)
+
+
 PROTO_TOL = {"fp32": 1e-4, "fp16": 8e-4, "bf16": 6e-3}  # ~3x the MI355X drift (profiles/r2/parity_yolact.json)
 
 

@@ -9,6 +9,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "tauv-vision_amd")]
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+bench.forward_env_knobs(bench.env_knobs())
 import tauv_vision_amd as tv  # noqa: E402
 
 prec = sys.argv[1] if len(sys.argv) > 1 else "fp16"

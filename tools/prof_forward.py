@@ -10,7 +10,8 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from bench import build_model  # noqa: E402
+from bench import build_model, env_knobs, forward_env_knobs  # noqa: E402
+forward_env_knobs(env_knobs())
 
 
 def main():

@@ -89,6 +89,7 @@ struct ConvParams {
   const float* head_b;  // [ntiles][32] 1x1 bias on the first tile of each head, zeros elsewhere
   int head_ldc;
   int head_row0[16], head_nrows[16];
+  unsigned long long* dbg;  // diagnostic stamp builds only (conv3x3 TV_C3_EXP == 9): per-wave cycle buckets
 };
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.

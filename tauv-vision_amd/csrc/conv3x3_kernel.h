@@ -39,6 +39,28 @@
 #pragma once
 #include "conv_common.h"
 
+#ifndef TV_C3_EXP
+#define TV_C3_EXP 0  // diagnostic builds (tools/gpu_libab.sh): 2 = no epilogue stores, 3 = 16x16x32 MFMAs
+                     // (timing only, wrong results); 9 = per-wave cycle stamps into ConvParams.dbg
+#endif
+#if TV_C3_EXP == 9
+// s_memtime + lgkmcnt(0) as one statement (cdna_hip_programming.md §7, in-kernel stamps); the
+// cycles since the previous stamp go to bucket B
+#define C3_STAMP(B)                                                                    \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    unsigned long long t_;                                                             \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    st_b[B] += t_ - st_last;                                                           \
+    st_last = t_;                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#else
+#define C3_STAMP(B) \
+  do {              \
+  } while (0)
+#endif
+
 #include <type_traits>
 
 namespace tv {
@@ -199,6 +221,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   const int ntl = first < end ? UP * ((end - first + stride - 1) / stride) : 0;
   if (ntl == 0) return;
+#if TV_C3_EXP == 9
+  // buckets: 0 barrier (+ tap-8 vmcnt) wait, 1 first half-step (+ H1 drain), 2 second half-step
+  // (+ next H0 drain), 3 epilogue, 4 prologue, 5 k-steps
+  unsigned long long st_b[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long st_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
   const int S_tot = ntl * SPTK;
 
   // bias of every output channel into LDS (read in the epilogues)
@@ -369,6 +398,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   f32x16 acc[2][NI];  // [pixel fragment f][channel fragment i]; first written by a tile's first k-step
+#if TV_C3_EXP == 3
+  f32x4 acc4[2][NI][2];  // timing-only 16x16x32 accumulators (copied into acc before the epilogue)
+#endif
 
   // the 2 MFMAs of channel fragment I of one sub-step; FIRST: the tile's first products
   // (accumulate onto zero instead of clearing the accumulators in the epilogue)
@@ -378,13 +410,34 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       acc[0][I] = f32x16{};
       acc[1][I] = f32x16{};
     }
+#if TV_C3_EXP == 3  // timing only: the same MACs as two 16x16x32 MFMAs each (wrong results)
+    if constexpr (decltype(first)::value) {
+      acc4[0][I][0] = acc4[0][I][1] = acc4[1][I][0] = acc4[1][I][1] = f32x4{};
+    }
+    acc4[0][I][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, to_u4(F.w[I])), __builtin_bit_cast(half8, to_u4(F.x[0])), acc4[0][I][0], 0, 0, 0);
+    acc4[1][I][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, to_u4(F.w[I])), __builtin_bit_cast(half8, to_u4(F.x[1])), acc4[1][I][0], 0, 0, 0);
+    acc4[0][I][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, to_u4(F.x[0])), __builtin_bit_cast(half8, to_u4(F.w[I])), acc4[0][I][1], 0, 0, 0);
+    acc4[1][I][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, to_u4(F.x[1])), __builtin_bit_cast(half8, to_u4(F.w[I])), acc4[1][I][1], 0, 0, 0);
+#else
     Mfma<T>::run(to_u4(F.w[I]), to_u4(F.x[0]), acc[0][I]);
     Mfma<T>::run(to_u4(F.w[I]), to_u4(F.x[1]), acc[1][I]);
+#endif
   };
 
   // ---- epilogue of the tile (fr, y0, x0, nt): straight from the accumulators
   auto epilogue = [&](int fr, int y0, int x0, int nt, int hsel) __attribute__((always_inline)) {
     const int n0 = nt * BNK;
+#if TV_C3_EXP == 3
+#pragma unroll
+    for (int f = 0; f < 2; ++f)
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[f][i][e] = acc4[f][i][0][e];
+          acc[f][i][4 + e] = acc4[f][i][1][e];
+        }
+#endif
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       const int q = WP * wave + 32 * f + l32;
@@ -429,6 +482,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
             const unsigned b0 = pack2<OutT>(v[1][0], v[1][1]), b1 = pack2<OutT>(v[1][2], v[1][3]);
             const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
             const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+#if TV_C3_EXP == 2  // timing only: the tile's stores dropped (zero-size resource)
+            orsrc.z = 0;
+#endif
             raw_buffer_store_v4(u32x4{r0[0], r1[0], r0[1], r1[1]}, orsrc,
                                 ch < p.N ? (int)(obase + (unsigned)((32 * i + 16 * m) * sizeof(OutT))) : (int)0x80000000u, 0, 0);
           } else {
@@ -557,6 +613,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
   }
 
+  C3_STAMP(4);
   int s = 0;   // global k-step
   int tl = 0;  // tile index within this block's list
   int cb = 0;  // channel block within the tile (compile-time inside cblock)
@@ -580,6 +637,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     //  * tap 8 with RES: the residual step reads this block's residual input (last piece at
     //    tap 4): younger = weight loads of taps 4, 5, 6, 7 + the tap-5 halo piece.
     static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
+    C3_STAMP(2);
+#if TV_C3_EXP == 9
+    st_b[5] += 1;
+#endif
     auto wl = [&](int q) { return q >= 0 ? 1 : 0; };
     if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
@@ -587,6 +648,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    C3_STAMP(0);
 
     constexpr int NTAP = TAP == 8 ? (RES ? 9 : 0) : TAP == 9 ? 0 : TAP + 1;
     const bool do_r = s + 1 < S_tot;
@@ -629,6 +691,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       mfma_pair(IC<3>{}, IC<FIRST>{}, H0);
     }
     __builtin_amdgcn_sched_barrier(0);
+    C3_STAMP(1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
     __builtin_amdgcn_sched_barrier(0);
     mfma_pair(IC<0>{}, IC<false>{}, H1);
@@ -694,16 +757,28 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
   for (; tl < ntl;) {
     blocks(blocks, IC<0>{}, IC<0>{});
+    C3_STAMP(2);
     epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
+    C3_STAMP(3);
     ++tl;
     if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
     if constexpr (UP == 2) {  // the pair's second unit (ntl is even)
       blocks(blocks, IC<0>{}, IC<1>{});
+      C3_STAMP(2);
       epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
+      C3_STAMP(3);
       ++tl;
       if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
     }
   }
+#if TV_C3_EXP == 9
+  if (p.dbg && lane == 0) {
+    unsigned long long* d = p.dbg + ((size_t)blockIdx.x * NW + wave) * 8;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d[k] = st_b[k];
+    d[6] = (unsigned long long)ntl;
+  }
+#endif
 }
 
 template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4, int NCB = 4>

@@ -314,6 +314,11 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_C3_NI") c3_ni_force = v == 2 ? 2 : v == 4 ? 4 : 0;
     else if (k == "TV_C3_HALF_COST") c3_half_cost = v;
     else if (k == "TV_SLICES") slices = std::max(1, std::min(kMaxSlices, v));
+    else if (k == "TV_C3_STAMPS") {  // "op:device pointer" (stamp builds of conv3x3 only)
+      stamp_op = v;
+      const char* c = std::strchr(env, ':');
+      stamp_buf = c ? reinterpret_cast<unsigned long long*>(std::strtoull(c + 1, nullptr, 0)) : nullptr;
+    }
     else if (k == "TV_SLICE_SIZES") {
       for (const char* c = env; *c;) {
         slice_sizes_env.push_back(std::atoi(c));
@@ -771,6 +776,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->s2_grid[i] = 0;
     ws->lat[i] = 1;
   }
+  if (stamp_op >= 0 && stamp_op < (int)plan.ops.size() && ws->c3_tw[stamp_op]) ws->params[stamp_op].dbg = stamp_buf;
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));

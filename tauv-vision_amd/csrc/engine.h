@@ -75,6 +75,8 @@ struct Engine {
                                // (env TV_LAT=0 off)
   int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (env TV_DCN64=0 off)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
+  int stamp_op = -1;           // diagnostics: op whose conv3x3 launch gets a stamp buffer (knob TV_C3_STAMPS=op:ptr)
+  unsigned long long* stamp_buf = nullptr;
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1
   // concurrent slices: a batch of >= slices * slice_min frames runs as `slices` near-equal parts,

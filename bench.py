@@ -88,13 +88,47 @@ class Pipeline:
         return self.dec(p.heatmap, p.size, p.offset, p.depth, 0, self.mc.downsample_ratio, self.mc.in_h,
                         self.mc.in_w, self.thr)
 
-    def step(self, frames, gather=None):
+    def compute(self, frames):
         self.eng.forward_u8(frames, self.out)
-        rec, cnt = self.decode()
+        return self.decode()
+
+    def finish(self, rec, cnt, gather=None):
         if gather is not None:
-            gather(rec, cnt)
+            gather(rec, cnt)  # every rank's records into the gather buffers (RCCL all-gather)
         self.host.copy_(rec, non_blocking=True)
         self.host_counts.copy_(cnt, non_blocking=True)
+
+    def step(self, frames, gather=None):
+        rec, cnt = self.compute(frames)
+        self.finish(rec, cnt, gather)
+
+
+class GraphStep:
+    """The step as one hipGraph (torch.cuda.CUDAGraph): forward_u8 (two concurrent slices, their
+    fork / join events captured) + decode + D2H of the records; with N ranks the RCCL all-gather
+    and the D2H run eagerly after the replay. The pipeline's workspaces are keyed to the capture
+    stream (prepared by an eager warm-up on it); tests/test_gpu_capture.py checks replay == eager
+    bit for bit."""
+
+    def __init__(self, pipe, frames, gather, device):
+        self.pipe, self.frames, self.gather = pipe, frames, gather
+        self.stream = torch.cuda.Stream(device)
+        self.stream.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(self.stream):
+            for _ in range(2):
+                pipe.step(frames, gather)
+        torch.cuda.current_stream(device).wait_stream(self.stream)
+        torch.cuda.synchronize(device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=self.stream):
+            self.rec, self.cnt = pipe.compute(frames)
+            if gather is None:
+                pipe.finish(self.rec, self.cnt)
+
+    def __call__(self):
+        self.graph.replay()
+        if self.gather is not None:
+            self.pipe.finish(self.rec, self.cnt, self.gather)
 
 
 def timed(fn, steps, warmup, world=1, device=None):
@@ -595,6 +629,8 @@ def main():
     ap.add_argument("--b1-steps", type=int, default=200)
     ap.add_argument("--fp32-steps", type=int, default=3)
     ap.add_argument("--allow-env-knobs", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch the timed step eagerly instead of replaying it as one hipGraph")
     ap.add_argument("--cpu-dryrun", action="store_true",
                     help="CPU/gloo check of the --gpus N launcher, frame sharding and record all-gather (no kernels)")
     ap.add_argument("--model", default="r18", choices=["r18", "dla34", "yolact"],
@@ -630,13 +666,25 @@ def main():
     mc = tv.ModelConfig(HEIGHTS, CHANNELS, H, W, DOWNSAMPLES, 1.0)
     gen = torch.Generator(device=device).manual_seed(1000 + rank)
     frames = torch.randint(0, 256, (B, H, W, 3), generator=gen, device=device, dtype=torch.uint8)
-    pipe = Pipeline(model, oc, mc, B, K, args.thr, device)
-
     # detections of every rank on every rank: one RCCL all-gather of the packed records
     gather = RecordGather(B, K, device) if world > 1 else None
-    elapsed = timed(lambda: pipe.step(frames, gather), args.steps, args.warmup, world, device)
+    launch = "eager"
+    eager_value = None
+    if args.eager:
+        pipe = Pipeline(model, oc, mc, B, K, args.thr, device)
+        step = lambda: pipe.step(frames, gather)  # noqa: E731
+    else:
+        side = torch.cuda.Stream(device)
+        with torch.cuda.stream(side):  # workspaces keyed to the capture stream
+            pipe = Pipeline(model, oc, mc, B, K, args.thr, device)
+        step = GraphStep(pipe, frames, gather, device)
+        launch = "hipGraph replay"
+    elapsed = timed(step, args.steps, args.warmup, world, device)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
+    if not args.eager:  # the same step launched eagerly, for comparison (same buffers)
+        el_e = timed(lambda: pipe.step(frames, gather), args.steps, 2, world, device)
+        eager_value = round(world * B * args.steps / el_e, 2)
     gathered = int(gather.rec.shape[0] * gather.rec.shape[1]) if gather is not None else B
     ranks = dist.get_world_size() if world > 1 else 1
     if world > 1:
@@ -684,6 +732,7 @@ def main():
                                                                   f"detections)" if world > 1 else "dp1"},
             "e2e_tflops": round(value * flops_frame / 1e12, 2),
             "e2e_frac_of_peak": round(value * flops_frame / 1e12 / PEAK_TFLOPS[args.precision], 4),
+            "launch": launch, "eager_value": eager_value,
             "roofline": roof, "latency_b1": b1, "cpu_baseline": cpu,
         }
         line.update(extras)

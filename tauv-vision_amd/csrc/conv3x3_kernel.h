@@ -224,7 +224,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 #if TV_C3_EXP == 9
   // buckets: 0 barrier (+ tap-8 vmcnt) wait, 1 first half-step (+ H1 drain), 2 second half-step
   // (+ next H0 drain), 3 epilogue, 4 prologue, 5 k-steps
-  unsigned long long st_b[6] = {0, 0, 0, 0, 0, 0};
+  // 6 tap-8 vmcnt wait (next block's halo), 7 the barrier after it
+  unsigned long long st_b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_last;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
@@ -614,6 +615,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
 
   C3_STAMP(4);
+  // static priority for the second-dispatched half (waves 4-7, the SIMD partners of waves 0-3):
+  // the arbitration loser on every segment otherwise (MI355X_MICROARCH.md, two waves per SIMD,
+  // item 4). Measured: 60x80 layers -3%, the others -0.4..-1%
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   int s = 0;   // global k-step
   int tl = 0;  // tile index within this block's list
   int cb = 0;  // channel block within the tile (compile-time inside cblock)
@@ -645,10 +650,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
     if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
+    if constexpr (TAP >= 8) C3_STAMP(6);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if TV_C3_EXP == 4  // timing only: barrier only at tap 8 (wrong results)
+    if constexpr (TAP >= 8) __builtin_amdgcn_s_barrier();
+#else
     __builtin_amdgcn_s_barrier();
+#endif
     __builtin_amdgcn_sched_barrier(0);
-    C3_STAMP(0);
+    C3_STAMP(TAP >= 8 ? 7 : 0);
 
     constexpr int NTAP = TAP == 8 ? (RES ? 9 : 0) : TAP == 9 ? 0 : TAP + 1;
     const bool do_r = s + 1 < S_tot;
@@ -669,7 +679,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     read_one(IC<3>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     // k-step s+2 (loaded at step s-3) into its ring slot: it last held k-step s-1, read
     // completely before this step's barrier (past the end: an unread slot)
+#if TV_C3_EXP != 6  // 6: timing only, no weight ds_write (wrong results)
     *reinterpret_cast<WReg*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wvoff) = wreg[(PAR + 2) & 3];
+#endif
     if constexpr (TAP == 0) {
       if (nxt_exists && nxt_newtile) {
         int fr, y0, x0, nt;
@@ -684,7 +696,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       read_one(IC<5>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     }
     if constexpr (TAP < HTAPS)
+#if TV_C3_EXP != 5  // 5: timing only, no halo DMA in the main loop (wrong results)
       halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);  // (no next block: the idle buffer)
+#endif
     if constexpr (RES && TAP >= 1 && TAP <= RPW) res_piece(TAP - 1, cur_fr, cur_y0, cur_x0, cb);
     if constexpr (NI == 4) {
       __builtin_amdgcn_sched_barrier(0);
@@ -775,8 +789,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   if (p.dbg && lane == 0) {
     unsigned long long* d = p.dbg + ((size_t)blockIdx.x * NW + wave) * 8;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) d[k] = st_b[k];
-    d[6] = (unsigned long long)ntl;
+    for (int k = 0; k < 8; ++k) d[k] = st_b[k];
   }
 #endif
 }

@@ -15,7 +15,9 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 
-NAMES = ["barrier+vm wait", "first half (+H1 drain)", "second half (+H0 drain)", "epilogue", "prologue", "k-steps"]
+NAMES = ["barrier (taps 0-7)", "first half (+H1 drain)", "second half (+H0 drain)", "epilogue", "prologue", "k-steps",
+         "tap-8 halo vmcnt wait", "tap-8 barrier"]
+TIME = [0, 1, 2, 3, 4, 6, 7]
 
 
 def main():
@@ -46,15 +48,13 @@ def main():
         torch.cuda.synchronize()
         v = buf.view(256 * 8, 8).cpu()
         used = v[v[:, 5] > 0].double()
-        tot = used[:, :5].sum(1)
-        share = (used[:, :5].sum(0) / tot.sum()).tolist()
+        tot = used[:, TIME].sum(1)
         steps = float(used[:, 5].mean())
-        cyc_per_step = float((used[:, :3].sum(1) / used[:, 5]).mean())
         res.append({"op": ops[i][0], "kernel": ops[i][3], "ms_stamped": round(prof[i][1], 4), "waves": int(used.shape[0]),
-                    "share": {n: round(x, 4) for n, x in zip(NAMES, share)}, "k_steps_per_wave": steps,
-                    "cycles_per_kstep": round(cyc_per_step, 1),
-                    "bucket_cycles_per_kstep": {n: round(float((used[:, k] / used[:, 5]).mean()), 1)
-                                                for k, n in enumerate(NAMES[:4])}})
+                    "share": {NAMES[k]: round(float(used[:, k].sum() / tot.sum()), 4) for k in TIME},
+                    "k_steps_per_wave": steps,
+                    "cycles_per_kstep": round(float((tot / used[:, 5]).mean()), 1),
+                    "bucket_cycles_per_kstep": {NAMES[k]: round(float((used[:, k] / used[:, 5]).mean()), 1) for k in TIME}})
         set_diagnostic_knobs({})
     print(json.dumps(res, indent=1))
 

@@ -215,6 +215,27 @@ int tv_yolact_assemble_masks_indexed(const float* mask_prototype, const int64_t 
                                      int32_t A, const int64_t* det, const int32_t* counts, int32_t n_max, float* mask,
                                      void* stream);
 
+/* Training targets of the CenterNet loss (loss.py:31-135), fp32, device pointers, async on `stream`.
+ * generate_heatmap (loss.py:31-72): valid [B,n_objects] u8 (bool), label [B,n_objects] int64,
+ *   center [B,n_objects,2] fp32 (y, x normalised) -> heatmap [B,n_labels,in_h/ratio,in_w/ratio]:
+ *   per valid object exp(-((x-cx)^2 + (y-cy)^2) / (2 sigma^2)) maxed into its label's plane, with
+ *   (cy, cx) = floor(center * in / ratio) and sigma = max(sigma, 0.1) (the reference passes
+ *   TrainConfig.keypoint_heatmap_sigma); nan_to_num. A label outside [0, n_labels) is skipped
+ *   (the Python wrapper raises IndexError first, like the reference's indexing). */
+int tv_train_heatmap(const uint8_t* valid, const int64_t* label, const float* center, int32_t B, int32_t n_objects,
+                     int32_t n_labels, int32_t in_h, int32_t in_w, int32_t downsample_ratio, double sigma,
+                     float* heatmap, void* stream);
+/* generate_keypoint_heatmap (loss.py:75-135): keypoint instances [B,n_instances] (valid u8, label
+ * int64, center fp32 x2, owning object index int64 into center [B,n_objects,2]) -> heatmap and
+ * affinity_weight [B,n_keypoints,H,W] (Gaussians of heatmap_sigma / affinity_sigma, max), affinity
+ * [B,n_keypoints,2,H,W] (unit displacement from the owning object's center to each cell, of the
+ * instance nearest to that cell; the earliest instance wins ties); nan_to_num of all three. */
+int tv_train_keypoint_targets(const uint8_t* keypoint_valid, const int64_t* keypoint_label,
+                              const float* keypoint_center, const int64_t* keypoint_object_index, const float* center,
+                              int32_t B, int32_t n_instances, int32_t n_objects, int32_t n_keypoints, int32_t in_h,
+                              int32_t in_w, int32_t downsample_ratio, double heatmap_sigma, double affinity_sigma,
+                              float* heatmap, float* affinity_weight, float* affinity, void* stream);
+
 /* Diagnostics (GPU tests): one DeformConv2d(x, offset, sigmoid(mask)) (DeformConv.forward,
  * centerpoint_dla.py:389-391: 3x3, stride 1, pad 1) + bias + activation (0 none, 1 ReLU, 2 leaky)
  * through the kernel the engine uses for DLA-34's DeformConv layers. x: compute-dtype NHWC

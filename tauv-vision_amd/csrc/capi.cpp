@@ -373,4 +373,27 @@ int tv_diag_dcn_conv(const void* x, const void* om, int32_t B, int32_t H, int32_
                                       (hipStream_t)stream); })
 }
 
+int tv_train_heatmap(const uint8_t* valid, const int64_t* label, const float* center, int32_t B, int32_t n_objects,
+                     int32_t n_labels, int32_t in_h, int32_t in_w, int32_t downsample_ratio, double sigma,
+                     float* heatmap, void* stream) {
+  TV_GUARD({
+    return tv::launch_train_heatmap(valid, reinterpret_cast<const long long*>(label), center, B, n_objects, n_labels,
+                                    in_h, in_w, downsample_ratio, sigma, heatmap, (hipStream_t)stream);
+  })
+}
+
+int tv_train_keypoint_targets(const uint8_t* keypoint_valid, const int64_t* keypoint_label,
+                              const float* keypoint_center, const int64_t* keypoint_object_index, const float* center,
+                              int32_t B, int32_t n_instances, int32_t n_objects, int32_t n_keypoints, int32_t in_h,
+                              int32_t in_w, int32_t downsample_ratio, double heatmap_sigma, double affinity_sigma,
+                              float* heatmap, float* affinity_weight, float* affinity, void* stream) {
+  TV_GUARD({
+    return tv::launch_train_keypoints(keypoint_valid, reinterpret_cast<const long long*>(keypoint_label),
+                                      keypoint_center, reinterpret_cast<const long long*>(keypoint_object_index),
+                                      center, B, n_instances, n_objects, n_keypoints, in_h, in_w, downsample_ratio,
+                                      heatmap_sigma, affinity_sigma, heatmap, affinity_weight, affinity,
+                                      (hipStream_t)stream);
+  })
+}
+
 }  // extern "C"

@@ -147,6 +147,12 @@ struct DcnParams {
 };
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad);
 int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, hipStream_t s);  // dcn64_mode: 64-channel k-steps when C % 64 == 0
+// targets.hip: training targets of the loss (loss.py:31-135)
+int launch_train_heatmap(const uint8_t* valid, const long long* label, const float* center, int B, int n_obj, int L,
+                         int in_h, int in_w, int ratio, double sigma, float* out, hipStream_t s);
+int launch_train_keypoints(const uint8_t* kvalid, const long long* klabel, const float* kcenter, const long long* kobj,
+                           const float* center, int B, int n_inst, int n_obj, int K, int in_h, int in_w, int ratio,
+                           double heat_sigma, double aff_sigma, float* heat, float* aw, float* aff, hipStream_t s);
 // diag.cpp: one DeformConv2d + bias + activation through a chosen DCN kernel (GPU tests)
 int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int om_ldc, const float* weight,
                   const float* bias, int N, int act, int dtype, int variant, void* out, hipStream_t s);

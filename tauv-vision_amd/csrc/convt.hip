@@ -20,10 +20,6 @@
 //    mode-1 epilogue: (acc + bias) + skip.
 #include "conv_common.h"
 
-#ifndef TV_CT_EXP
-#define TV_CT_EXP 0  // timing-only experiment builds: 1 = whole-row skip loads / output stores (wrong data)
-#endif
-
 namespace tv {
 namespace convt {
 
@@ -128,17 +124,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     for (int j = 0; j < KJ; ++j) S.x[j] = gload16(src + 16 * j);
   };
   auto load_a = [&](int t, int ph, ASet& S) __attribute__((always_inline)) {
-#if TV_CT_EXP == 1  // timing only: each instruction reads 4 pixels' whole 256-byte rows (wrong data)
-    const long long tg = target(t, ph) - l32 + (lane >> 4);
-    const T* add = reinterpret_cast<const T*>(p.add) + (tg < 0 ? 0 : tg) * p.add_ldc + 8 * (lane & 15);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) S.a[q] = gload16(add + 8 * q * p.add_ldc);
-#else
     const long long tg = target(t, ph);
     const T* add = reinterpret_cast<const T*>(p.add) + (tg < 0 ? 0 : tg) * p.add_ldc + 8 * lh;
 #pragma unroll
     for (int q = 0; q < 8; ++q) S.a[q] = gload16(add + 16 * q);  // q = 2i + m -> channel 16q + 8lh
-#endif
   };
 
   auto compute_store = [&](int t, int ph, const XSet& X, const ASet& A) __attribute__((always_inline)) {
@@ -189,16 +178,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
           const unsigned sw[4] = {sk.x, sk.y, sk.z, sk.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = pack2<T>(lo_f<T>(sw[e]) + f[2 * e], hi_f<T>(sw[e]) + f[2 * e + 1]);
-#if TV_CT_EXP == 1
-          {
-            const long long tq = tg - l32 + (lane >> 4);
-            if (tq >= 0)
-              gstore16(reinterpret_cast<T*>(p.out) + (tq + 8 * (2 * i + m)) * p.out_ldc + 8 * (lane & 15),
-                       make_uint4(o[0], o[1], o[2], o[3]));
-          }
-#else
           if (tg >= 0) gstore16(out + 32 * i + 16 * m + 8 * lh, make_uint4(o[0], o[1], o[2], o[3]));
-#endif
         }
       }
     }

@@ -69,7 +69,7 @@ struct Engine {
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)
   int cu_count = 256;          // compute units (persistent grids)
   int headfuse_mode = 1;       // fuse the 1x1 heads into the 3x3 heads epilogue (env TV_HEADFUSE=0 off)
-  int convt_mode = 1;          // convt.hip for eligible fp16/bf16 up-paths (env TV_CONVT=0 off)
+  int convt_mode = 1;          // convt.hip for eligible fp16/bf16 up-paths (knob TV_CONVT=0 off)
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
   int lat_mode = 1;            // conv_lat.hip for layers whose chosen kernel fills < lat_units work units
                                // (env TV_LAT=0 off)

@@ -68,6 +68,9 @@ EXPORTS = {
                                   c_vp, c_vp], c_i32),
     "tv_yolact_assemble_masks_indexed": ([c_vp, ctypes.POINTER(c_i64), c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32,
                                           c_vp, c_vp, c_i32, c_vp, c_vp], c_i32),
+    "tv_train_heatmap": ([c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_f64, c_vp, c_vp], c_i32),
+    "tv_train_keypoint_targets": ([c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32,
+                                   c_f64, c_f64, c_vp, c_vp, c_vp, c_vp], c_i32),
     "tv_diag_dcn_conv": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                           c_vp, c_vp], c_i32),
     "tv_last_error": ([], ctypes.c_char_p),

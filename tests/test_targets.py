@@ -1,0 +1,87 @@
+"""Training targets (reference loss.py:31-135): the oracle restatement against
+the reference's own outputs (tests/golden/targets_*.npz, made by gen_golden_targets.py), and the
+HIP kernels (tv_train_heatmap / tv_train_keypoint_targets through tauv_vision_amd.loss) against
+both. The Gaussians are fp32 exp of fp32 arguments formed exactly as the reference forms them:
+the GPU exp may differ from torch's CPU exp by an ulp, so those planes are compared at 2e-7
+absolute (values in [0, 1]); the center cells, the winning instance per cell and the affinity
+vectors are exact arithmetic and compared at 1e-7 (one rounding of a quotient)."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import golden
+from oracle import ref_targets as rt
+
+CASES = ["targets_b2_o5_l3_240x320", "targets_b3_o9_l4_480x640", "targets_b2_o4_l2_96x128_tinysigma"]
+
+
+def _truth(g):
+    t = lambda k: torch.from_numpy(g[k])  # noqa: E731
+    return types.SimpleNamespace(valid=t("valid"), label=t("label"), center=t("center"),
+                                 keypoint_valid=t("keypoint_valid"), keypoint_label=t("keypoint_label"),
+                                 keypoint_center=t("keypoint_center"),
+                                 keypoint_object_index=t("keypoint_object_index"))
+
+
+def _configs(g):
+    import tauv_vision_amd as tv
+    mc = tv.ModelConfig([2] * 5, [16] * 6, int(g["in_h"]), int(g["in_w"]), int(g["downsamples"]), 1.0)
+    tc = types.SimpleNamespace(keypoint_heatmap_sigma=float(g["keypoint_heatmap_sigma"]),
+                               keypoint_affinity_sigma=float(g["keypoint_affinity_sigma"]))
+    return mc, tc
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_targets_match_reference(name):
+    g = golden(name)
+    mc, tc = _configs(g)
+    truth = _truth(g)
+    heat = rt.generate_heatmap(truth, mc, tc, int(g["n_labels"]))
+    np.testing.assert_array_equal(heat.numpy(), g["heatmap"])
+    kh, kaw, kaff = rt.generate_keypoint_heatmap(truth, mc, tc, int(g["n_keypoints"]))
+    np.testing.assert_array_equal(kh.numpy(), g["keypoint_heatmap"])
+    np.testing.assert_array_equal(kaw.numpy(), g["keypoint_affinity_weight"])
+    np.testing.assert_array_equal(kaff.numpy(), g["keypoint_affinity"])
+    np.testing.assert_array_equal(rt.out_index_for_position(truth.center, mc).numpy(), g["out_index"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_targets_match_reference(name):
+    from tauv_vision_amd import loss as L
+    g = golden(name)
+    mc, tc = _configs(g)
+    t = lambda k: torch.from_numpy(g[k]).cuda()  # noqa: E731
+    truth = L.PoseSample(valid=t("valid"), label=t("label"), center=t("center"), keypoint_valid=t("keypoint_valid"),
+                         keypoint_label=t("keypoint_label"), keypoint_center=t("keypoint_center"),
+                         keypoint_object_index=t("keypoint_object_index"))
+    oc = types.SimpleNamespace(n_labels=int(g["n_labels"]), n_keypoints=int(g["n_keypoints"]))
+    heat = L.generate_heatmap(truth, mc, tc, oc)
+    assert heat.is_cuda and heat.dtype == torch.float32
+    np.testing.assert_allclose(heat.cpu().numpy(), g["heatmap"], rtol=0, atol=2e-7)
+    kh, kaw, kaff = L.generate_keypoint_heatmap(truth, mc, tc, oc)
+    np.testing.assert_allclose(kh.cpu().numpy(), g["keypoint_heatmap"], rtol=0, atol=2e-7)
+    np.testing.assert_allclose(kaw.cpu().numpy(), g["keypoint_affinity_weight"], rtol=0, atol=2e-7)
+    np.testing.assert_allclose(kaff.cpu().numpy(), g["keypoint_affinity"], rtol=0, atol=1e-7)
+    # the Gaussian peaks (value 1 exactly at the center cell) land on the same cells
+    np.testing.assert_array_equal(heat.cpu().numpy() == 1.0, g["heatmap"] == 1.0)
+    np.testing.assert_array_equal(L.out_index_for_position(truth.center, mc).cpu().numpy(), g["out_index"])
+
+
+@pytest.mark.gpu
+def test_gpu_targets_empty_and_all_invalid():
+    from tauv_vision_amd import loss as L
+    import tauv_vision_amd as tv
+    mc = tv.ModelConfig([2] * 5, [16] * 6, 64, 96, 1, 1.0)
+    tc = types.SimpleNamespace(keypoint_heatmap_sigma=2.0, keypoint_affinity_sigma=3.0)
+    oc = types.SimpleNamespace(n_labels=2, n_keypoints=2)
+    z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device="cuda")  # noqa: E731
+    for n in (0, 3):  # no objects at all / every object and instance invalid
+        truth = L.PoseSample(valid=z(2, n, dt=torch.bool), label=z(2, n, dt=torch.int64), center=z(2, n, 2),
+                             keypoint_valid=z(2, n, dt=torch.bool), keypoint_label=z(2, n, dt=torch.int64),
+                             keypoint_center=z(2, n, 2), keypoint_object_index=z(2, n, dt=torch.int64))
+        assert float(L.generate_heatmap(truth, mc, tc, oc).abs().sum()) == 0.0
+        kh, kaw, kaff = L.generate_keypoint_heatmap(truth, mc, tc, oc)
+        assert float(kh.abs().sum() + kaw.abs().sum() + kaff.abs().sum()) == 0.0

@@ -124,7 +124,9 @@ int launch_conv3x3s2(const ConvParams& p, const ConvParams* dp, void* out, int d
 // k-step-major, pre-swizzled weight copy the kernel streams (from the [Npad][Kpad] packing)
 // (ncb = input channel blocks of 32: 4 for 128-channel inputs, 8 for 256)
 size_t conv3x3_weight_bytes(int ntiles, int res, int ncb);
-int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, void* out, hipStream_t s);
+int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, int k16, void* out, hipStream_t s);
+// whether the conv3x3 instance (epi, res, ni) runs the 16x16x32 body (its weights use that body's swizzle)
+int conv3x3_k16(int epi, int res, int ni);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,

@@ -61,10 +61,65 @@
   } while (0)
 #endif
 
+#ifndef TV_C3_MF
+#define TV_C3_MF 16  // MFMA shape of the plain NI 4 tile body (K16): 16 = v_mfma_f32_16x16x32, 32 = 32x32x16
+#endif
+
 #include <type_traits>
 
 namespace tv {
 namespace c3 {
+
+// 16x16x32 body (M16): a k-step (one tap x 32 channels) is ONE K=32 MFMA step; a wave's 64 pixels are
+// 4 fragments of 16 and its 128 channels 8 fragments of 16 (32 MFMAs per k-step, as 16 of 32x32x16).
+// Lane l = 16c + n supplies fragment row/column n and K group c, which reads the 16-byte chunk
+// sigma(c) = (0, 2, 1, 3)[c] of the 64-byte channel block, and fragment column n is pixel pi(n) of
+// the fragment: pi maps {0..3, 12..15} to the even and {4..11} to the odd pixels, so that the
+// ds_read_b128 lane groups hit 16 distinct 4-bank sets on the 80-byte-pitch halo; weight rows are
+// swizzled chunk ^ ((row >> 3) & 1) (wswz) (MI355X_MICROARCH.md LDS table; checked by tools/bank_check.py).
+constexpr bool M16 = TV_C3_MF == 16;
+__device__ __forceinline__ int m16_sigma(int c) { return ((c & 1) << 1) | (c >> 1); }
+__device__ __forceinline__ int m16_pi(int n) { return n < 4 ? 2 * n : n < 12 ? 2 * n - 7 : 2 * n - 16; }
+// host + device: the weight-row chunk swizzle of the LDS ring (and of the repacked weights)
+__host__ __device__ constexpr int wswz(int row, bool k16) { return k16 ? (row >> 3) & 1 : (row >> 2) & 3; }
+
+template <typename T> struct Mfma16;
+template <> struct Mfma16<_Float16> {
+  __device__ static void run(const uint4& a, const uint4& b, f32x4& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), acc, 0, 0, 0);
+  }
+};
+template <> struct Mfma16<__bf16> {
+  __device__ static void run(const uint4& a, const uint4& b, f32x4& acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+  }
+};
+
+// The main-loop 16x16x32 MFMAs as asm statements with the accumulator tied to C: through the
+// builtin, hipcc gave a third of them a fresh destination (an accumulator rotation across k-steps
+// that doubled the accumulator registers and spilled ~100 VGPRs). Hazards, placed by hand: every
+// accumulator's only in-loop reader is the next MFMA taking it whole as C (0 wait states); the
+// epilogue's first reader sits behind mfma16_drain() (8-pass XDL D -> VALU: 12 states); the A/B
+// operands come from ds_read_b128 behind counted lgkmcnt waits (no VALU producer).
+template <typename T, bool FIRST>
+__device__ __forceinline__ void mfma16_asm(f32x4& acc, const u32x4& a, const u32x4& b) {
+  if constexpr (FIRST) {
+    if constexpr (std::is_same<T, __bf16>::value)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+    else
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+  } else {
+    if constexpr (std::is_same<T, __bf16>::value)
+      asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+    else
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  }
+}
+__device__ __forceinline__ void mfma16_drain() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
 
 constexpr int NT = 512, NW = 8, BN = 128, P = 512;
 constexpr int WP = P / NW;                    // pixels per wave = 64 (two 32-pixel fragments)
@@ -170,6 +225,12 @@ __device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh
 template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI, int NCB>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
+  // The 16x16x32 body for the plain 128-channel-tile instances only. Measured (profiles/r3b): the
+  // dominant 120x160 layer 1.476 -> 1.423 ms per slice; the fused-heads epilogue on 16x16 tiles
+  // (16-pixel fragments, twice the head MFMAs' issue slots per pixel) 0.883 -> 0.950 ms; the
+  // half-tile (NI 2) instances +1-3%; the residual instances need ~12 VGPRs more than the 256 of
+  // two waves per SIMD.
+  constexpr bool K16 = M16 && !RES && EPI == 0 && NI == 4;
   static_assert(NI == 4 || (NI == 2 && EPI == 0), "half tiles: plain epilogue only");
   static_assert(!(EPI == 1 && RES), "fused heads use the residual LDS region for their 1x1 weights");
   constexpr int SPTK = spt<RES, NCB>();  // k-steps per tile
@@ -379,11 +440,28 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // RES: fragment base of pixel q0 = WP*wave + l32 in the residual buffer, per sub-step J
   // (fragment f = 1 is q0 + 32: +2 KiB, same swizzle)
   [[maybe_unused]] unsigned rxa[2];
-  if constexpr (RES) {
+  if constexpr (RES && !K16) {
     const int q0 = WP * wave + l32;
 #pragma unroll
     for (int j = 0; j < 2; ++j) rxa[j] = lds0 + OFF_R + (unsigned)(q0 * 64 + (((2 * j + lh) ^ ((q0 >> 2) & 3)) << 4));
   }
+
+  // ---- K16 fragment addresses: lane (c16, n16) reads chunk m16_sigma(c16) of pixel
+  // WP*wave + 16f + m16_pi(n16) (fragment f: a compile-time offset) / of weight row 16i + n16
+  const int n16 = lane & 15, c16 = lane >> 4;
+  [[maybe_unused]] const int pin = m16_pi(n16), sig = m16_sigma(c16);
+  [[maybe_unused]] unsigned xa16 = 0, wa16 = 0, rxa16 = 0;
+  if constexpr (K16) {
+    const int q = WP * wave + pin;
+    const int r = q / TW, c = q - (q / TW) * TW;
+    xa16 = lds0 + (unsigned)((r * RS + c) * PITCH + sig * 16);
+    wa16 = lds0 + OFF_W + (unsigned)(n16 * 64 + ((sig ^ wswz(n16, true)) << 4));
+    if constexpr (RES) rxa16 = lds0 + OFF_R + (unsigned)(q * 64 + ((sig ^ ((q >> 2) & 3)) << 4));
+  }
+  // pixel fragment f's offset from fragment 0 in the halo (TW 32: two 16-pixel halves of a row
+  // pair; TW 16: one row each)
+  constexpr int FO16[4] = {0, TW == 32 ? 16 * PITCH : RS * PITCH, TW == 32 ? RS * PITCH : 2 * RS * PITCH,
+                           TW == 32 ? (RS + 16) * PITCH : 3 * RS * PITCH};
 
   // read R (0..5) of sub-step J of a k-step: x[f] for R < 2, else w[i]; TAP 9 = residual k-step
   auto read_one = [&](auto r, auto j, auto tap, unsigned xb, unsigned wb, Half<NI>& F) __attribute__((always_inline)) {
@@ -399,6 +477,21 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   f32x16 acc[2][NI];  // [pixel fragment f][channel fragment i]; first written by a tile's first k-step
+  [[maybe_unused]] f32x4 a16[4][2 * NI];  // K16: [16-pixel fragment f][16-channel fragment i]
+  [[maybe_unused]] u32x4 X16[1][4];        // K16: the 4 pixel fragments of a k-step
+  [[maybe_unused]] u32x4 W16[2][NI];       // K16: channel fragments 0..NI-1 / NI..2NI-1 of a k-step
+
+  // K16: fragment reads (tap 9 = the residual k-step) and the 4 MFMAs of channel fragment I
+  [[maybe_unused]] auto rd_x16 = [&](auto f, auto tap, unsigned xb) __attribute__((always_inline)) {
+    constexpr int F = decltype(f)::value, TAP = decltype(tap)::value;
+    if constexpr (TAP == 9) return ds_read16<F * 1024>(rxa16);
+    else return ds_read16<((TAP / 3) * RS + (TAP % 3)) * PITCH + FO16[F]>(xb);
+  };
+  [[maybe_unused]] auto quad16 = [&](auto i, auto first, const u32x4& w, const u32x4 (&x)[4]) __attribute__((always_inline)) {
+    constexpr int I = decltype(i)::value;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) mfma16_asm<T, decltype(first)::value>(a16[f][I], w, x[f]);
+  };
 #if TV_C3_EXP == 3
   f32x4 acc4[2][NI][2];  // timing-only 16x16x32 accumulators (copied into acc before the epilogue)
 #endif
@@ -560,6 +653,53 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     }
   };
 
+  // ---- K16 epilogue: lane (c16, n16) holds channels 16i + 4c16 + e of pixel pin of fragment f.
+  // Per channel-fragment pair (2j, 2j+1) one v_permlane16_swap per dword gives every lane 8
+  // consecutive channels — rows c16 = 0..3 of the pair: 32j + {0, 16, 8, 24} — one 16-byte store
+  // (a pixel's 64 contiguous bytes per instruction).
+  [[maybe_unused]] const int cofs16 = 16 * (c16 & 1) + 8 * (c16 >> 1);
+  [[maybe_unused]] auto epilogue16 = [&](int fr, int y0, int x0, int nt) __attribute__((always_inline)) {
+    mfma16_drain();
+    const int n0 = nt * BNK;
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+      const int q = WP * wave + 16 * f + pin;
+      const int y = y0 + q / TW, x = x0 + q % TW;
+      const bool ok = y < H && x < W && fr < nframes;
+      i32x4 orsrc;
+      const unsigned long long a = (unsigned long long)out_ptr + (unsigned long long)fr * out_frame_bytes;
+      orsrc.x = (int)(unsigned)a;
+      orsrc.y = (int)(unsigned)(a >> 32);
+      orsrc.z = (int)out_frame_bytes;
+      orsrc.w = 0x00020000;
+      const unsigned obase = ok ? ((unsigned)(y * W + x) * (unsigned)p.out_ldc + (unsigned)(p.out_coff + n0 + cofs16)) * (unsigned)sizeof(OutT)
+                                : 0x80000000u;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        float v[2][4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(lbias + n0 + 32 * j + 16 * h + 4 * c16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float t = a16[f][2 * j + h][e] + bb[e];
+            if constexpr (ACT == 1) t = fmaxf(t, 0.0f);
+            else if constexpr (ACT == 2) t = fmaxf(t, 0.01f * t);
+            v[h][e] = t;
+          }
+        }
+        const unsigned a0 = pack2<T>(v[0][0], v[0][1]), a1 = pack2<T>(v[0][2], v[0][3]);
+        const unsigned b0 = pack2<T>(v[1][0], v[1][1]), b1 = pack2<T>(v[1][2], v[1][3]);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+        const u32x4 hv = u32x4{r0[0], r1[0], r0[1], r1[1]};
+        const int ch = n0 + 32 * j + cofs16;
+        raw_buffer_store_v4(hv, orsrc, ch < p.N ? (int)(obase + (unsigned)(32 * j * sizeof(OutT))) : (int)0x80000000u, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // bound the live set: one channel-fragment pair at a time
+      }
+    }
+  };
+
   // ---- prologue: halo of (tile 0, block 0), weights of k-steps 0..2
   int cur_fr, cur_y0, cur_x0, cur_nt;
   tile_of(0, cur_fr, cur_y0, cur_x0, cur_nt);
@@ -605,13 +745,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   __builtin_amdgcn_sched_barrier(0);
 
   Half<NI> H0, H1;  // sub-step 0 / 1 fragments
-  read_one(IC<0>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<1>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<2>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  read_one(IC<3>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-  if constexpr (NI == 4) {
-    read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
-    read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+  if constexpr (K16) {
+    X16[0][0] = rd_x16(IC<0>{}, IC<0>{}, xa16);
+    X16[0][1] = rd_x16(IC<1>{}, IC<0>{}, xa16);
+    X16[0][2] = rd_x16(IC<2>{}, IC<0>{}, xa16);
+    X16[0][3] = rd_x16(IC<3>{}, IC<0>{}, xa16);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) W16[0][i] = ds_read16<0>(wa16 + i * 1024);
+  } else {
+    read_one(IC<0>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+    read_one(IC<1>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+    read_one(IC<2>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+    read_one(IC<3>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+    if constexpr (NI == 4) {
+      read_one(IC<4>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+      read_one(IC<5>{}, IC<0>{}, IC<0>{}, xa, wa[0], H0);
+    }
   }
 
   C3_STAMP(4);
@@ -670,6 +819,79 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
     constexpr int PAR = decltype(par)::value;  // s % 4 (36 or 40 k-steps per tile: static)
+    if constexpr (K16) {
+      // first half: channel fragments 0..NI-1 (W16[0], read during the previous k-step) x the 4
+      // pixel fragments, channel-major; this k-step's fragments NI..2NI-1 go out first (W16[1] is
+      // free). Second half: W16[1] x the pixel fragments, pixel-major, so that each pixel fragment
+      // retires after its NI MFMAs and the next k-step's fragment is read into the same registers
+      // (one operand set live: 4 + 2 NI fragments, as the 32x32 body's two sub-step sets); the
+      // next k-step's channel fragments 0..NI-1 go into W16[0], free since the first half.
+      const unsigned x16n = xa16 + (NTAP == 0 ? hbuf : (cb & 1)) * HBUF;
+      const unsigned w16c = wa16 + (unsigned)((s % RING) * WSLOT);
+      const unsigned w16n = wa16 + (unsigned)(((s + 1) % RING) * WSLOT);
+      u32x4(&X)[4] = X16[0];
+      u32x4(&WA)[NI] = W16[0];
+      u32x4(&WB)[NI] = W16[1];
+      quad16(IC<0>{}, IC<FIRST>{}, WA[0], X);
+      WB[0] = ds_read16<NI * 1024>(w16c);
+      WB[1] = ds_read16<(NI + 1) * 1024>(w16c);
+      __builtin_amdgcn_sched_barrier(0);
+      quad16(IC<1>{}, IC<FIRST>{}, WA[1], X);
+      if constexpr (NI == 4) {
+        WB[2] = ds_read16<6 * 1024>(w16c);
+        WB[3] = ds_read16<7 * 1024>(w16c);
+      }
+#if TV_C3_EXP != 6
+      *reinterpret_cast<WReg*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wvoff) = wreg[(PAR + 2) & 3];
+#endif
+      if constexpr (TAP == 0) {
+        if (nxt_exists && nxt_newtile) {
+          int fr, y0, x0, nt;
+          tile_of(tl + 1, fr, y0, x0, nt);
+          halo_offsets(fr, y0, x0);
+        }
+      }
+      if constexpr (NI == 4) {
+        __builtin_amdgcn_sched_barrier(0);
+        quad16(IC<2>{}, IC<FIRST>{}, WA[2], X);
+      }
+      if constexpr (TAP < HTAPS) halo_piece(IC<TAP>{}, nxt_newtile ? 0 : cb + 1, hbuf);
+      if constexpr (RES && TAP >= 1 && TAP <= RPW) res_piece(TAP - 1, cur_fr, cur_y0, cur_x0, cb);
+      if constexpr (NI == 4) {
+        __builtin_amdgcn_sched_barrier(0);
+        quad16(IC<3>{}, IC<FIRST>{}, WA[3], X);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      C3_STAMP(1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // W16[1] landed
+      __builtin_amdgcn_sched_barrier(0);
+      auto group = [&](auto f) __attribute__((always_inline)) {  // pixel fragment F x W16[1]
+        constexpr int F = decltype(f)::value;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) mfma16_asm<T, FIRST>(a16[F][NI + i], WB[i], X[F]);
+      };
+      group(IC<0>{});
+      w_load(wreg[(PAR + 1) & 3]);
+      WA[0] = ds_read16<0>(w16n);
+      WA[1] = ds_read16<1024>(w16n);
+      X[0] = rd_x16(IC<0>{}, IC<NTAP>{}, x16n);
+      __builtin_amdgcn_sched_barrier(0);
+      group(IC<1>{});
+      if constexpr (NI == 4) {
+        WA[2] = ds_read16<2048>(w16n);
+        WA[3] = ds_read16<3072>(w16n);
+      }
+      X[1] = rd_x16(IC<1>{}, IC<NTAP>{}, x16n);
+      __builtin_amdgcn_sched_barrier(0);
+      group(IC<2>{});
+      X[2] = rd_x16(IC<2>{}, IC<NTAP>{}, x16n);
+      __builtin_amdgcn_sched_barrier(0);
+      group(IC<3>{});
+      X[3] = rd_x16(IC<3>{}, IC<NTAP>{}, x16n);
+      __builtin_amdgcn_sched_barrier(0);
+      ++s;
+      return;
+    }
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
     read_one(IC<0>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
     read_one(IC<1>{}, IC<1>{}, IC<TAP>{}, xc, wc1, H1);
@@ -772,14 +994,16 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   for (; tl < ntl;) {
     blocks(blocks, IC<0>{}, IC<0>{});
     C3_STAMP(2);
-    epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
+    if constexpr (K16) epilogue16(cur_fr, cur_y0, cur_x0, cur_nt);
+    else epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
     C3_STAMP(3);
     ++tl;
     if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);
     if constexpr (UP == 2) {  // the pair's second unit (ntl is even)
       blocks(blocks, IC<0>{}, IC<1>{});
       C3_STAMP(2);
-      epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
+      if constexpr (K16) epilogue16(cur_fr, cur_y0, cur_x0, cur_nt);
+      else epilogue(cur_fr, cur_y0, cur_x0, cur_nt, tl & 1);
       C3_STAMP(3);
       ++tl;
       if (tl < ntl) tile_of(tl, cur_fr, cur_y0, cur_x0, cur_nt);

@@ -354,6 +354,7 @@ Engine::~Engine() {
     if (p.w) (void)hipFree(p.w);
     if (p.w_c3) (void)hipFree(p.w_c3);
     if (p.w_c3h) (void)hipFree(p.w_c3h);
+    if (p.w_c3e) (void)hipFree(p.w_c3e);
     if (p.head_w) (void)hipFree(p.head_w);
     if (p.head_b) (void)hipFree(p.head_b);
     if (p.bias) (void)hipFree(p.bias);
@@ -602,7 +603,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
         void*& wc = ni == 4 ? pk3.w_c3 : pk3.w_c3h;
         if (!wc) {
           TV_HIP(hipMalloc(&wc, conv3x3_weight_bytes(p.ntiles, res, cs.C / 32)));
-          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, ni, cs.C / 32, wc, nullptr);
+          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, ni, cs.C / 32, conv3x3_k16(0, res, ni), wc, nullptr);
           if (rc) return rc;
           TV_HIP(hipDeviceSynchronize());
         }
@@ -697,6 +698,17 @@ int Engine::make_workspace(int B, Workspace* ws) {
         ws->params[i].ntiles != plan.ops[i].N / 128)
       continue;
     ConvParams& p = ws->params[i];
+    if (conv3x3_k16(1, 0, 4) != conv3x3_k16(0, 0, 4)) {  // the fused-heads body reads the other swizzle
+      Packed& pk3 = packed[i];
+      if (!pk3.w_c3e) {
+        const int ncb = plan.tensors[plan.ops[i].segs[0].src].C / 32;
+        TV_HIP(hipMalloc(&pk3.w_c3e, conv3x3_weight_bytes(p.ntiles, 0, ncb)));
+        int rc = conv3x3_repack(pk3.w, pk3.Kpad, dtype_size(dtype), p.ntiles, 0, 4, ncb, conv3x3_k16(1, 0, 4), pk3.w_c3e, nullptr);
+        if (rc) return rc;
+        TV_HIP(hipDeviceSynchronize());
+      }
+      p.weight = pk3.w_c3e;
+    }
     p.head_w = pk2.head_w;
     p.head_b = pk2.head_b;
     p.head_ldc = plan.out_cpad;

@@ -15,6 +15,7 @@ struct Packed {
   void* w = nullptr;       // [Npad][Kpad] compute dtype
   void* w_c3 = nullptr;    // conv3x3.hip / conv3x3s2.hip k-step-major copy (made on first use)
   void* w_c3h = nullptr;   // conv3x3.hip copy for 64-channel half tiles (ni = 2)
+  void* w_c3e = nullptr;   // conv3x3.hip copy for the fused-heads body when its swizzle differs (conv3x3_k16)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;

@@ -12,7 +12,9 @@
 //                 its length is strictly below the running minimum: the earliest instance
 //                 wins ties (:116-129)
 // Output planes are written once, coalesced (consecutive threads = consecutive cells). The
-// reference's exp is torch's CPU expf; this is the device expf (both ~1 ulp).
+// reference's exp is torch's CPU expf; this is the device expf (both ~1 ulp). The affinity's
+// sqrt and quotient are correctly rounded here; torch's CPU sqrt (MKL VML vsSqrt) returns one
+// ulp below the correctly rounded root for ~0.6% of fp32 inputs (tests/test_targets.py).
 #include "common.h"
 
 #include <cfloat>

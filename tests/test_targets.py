@@ -3,8 +3,11 @@ the reference's own outputs (tests/golden/targets_*.npz, made by gen_golden_targ
 HIP kernels (tv_train_heatmap / tv_train_keypoint_targets through tauv_vision_amd.loss) against
 both. The Gaussians are fp32 exp of fp32 arguments formed exactly as the reference forms them:
 the GPU exp may differ from torch's CPU exp by an ulp, so those planes are compared at 2e-7
-absolute (values in [0, 1]); the center cells, the winning instance per cell and the affinity
-vectors are exact arithmetic and compared at 1e-7 (one rounding of a quotient)."""
+absolute (values in [0, 1]). The affinity vectors are d / sqrt(d0^2 + d1^2): the reference's
+torch.sqrt on CPU is MKL VML's vsSqrt, which is not correctly rounded (measured here: 0.6% of
+fp32 results one ulp below the correctly rounded root, never above), while the kernel's sqrt
+and quotient are correctly rounded, so those planes are also compared at 2e-7 (values in
+[-1, 1]; a differently chosen winning instance would show as an O(1) error)."""
 import types
 
 import numpy as np
@@ -64,7 +67,7 @@ def test_gpu_targets_match_reference(name):
     kh, kaw, kaff = L.generate_keypoint_heatmap(truth, mc, tc, oc)
     np.testing.assert_allclose(kh.cpu().numpy(), g["keypoint_heatmap"], rtol=0, atol=2e-7)
     np.testing.assert_allclose(kaw.cpu().numpy(), g["keypoint_affinity_weight"], rtol=0, atol=2e-7)
-    np.testing.assert_allclose(kaff.cpu().numpy(), g["keypoint_affinity"], rtol=0, atol=1e-7)
+    np.testing.assert_allclose(kaff.cpu().numpy(), g["keypoint_affinity"], rtol=0, atol=2e-7)
     # the Gaussian peaks (value 1 exactly at the center cell) land on the same cells
     np.testing.assert_array_equal(heat.cpu().numpy() == 1.0, g["heatmap"] == 1.0)
     np.testing.assert_array_equal(L.out_index_for_position(truth.center, mc).cpu().numpy(), g["out_index"])

@@ -153,11 +153,12 @@ def timed(fn, steps, warmup, world=1, device=None):
     return elapsed
 
 
-def load_traffic(kernel, batch, precision):
+def load_traffic(kernel, batch, precision, model="r18"):
     """HBM bytes per launch of `kernel` from the committed PMC profile (tools/traffic.py over
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md),
-    or None when no profile of this exact workload is committed."""
-    path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md;
+    profiles/hbm_traffic.json for R18, hbm_traffic_<model>.json for the others), or None when no
+    profile of this exact workload is committed."""
+    path = os.path.join(ROOT, "profiles", "hbm_traffic.json" if model == "r18" else f"hbm_traffic_{model}.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -168,7 +169,7 @@ def load_traffic(kernel, batch, precision):
     return None if k is None else k["bytes_per_launch"]
 
 
-def conv_roofline(pipe, frames, precision, reps=3):
+def conv_roofline(pipe, frames, precision, reps=3, model="r18"):
     """Per-launch HIP-event timing of one forward (tv_engine_profile: events recorded on the
     launch stream around every launch; a separate pass after the timed region). The timed path
     launches a B-frame forward as concurrent slices (engine.slices), so the pass times one
@@ -207,7 +208,7 @@ def conv_roofline(pipe, frames, precision, reps=3):
             "frac": round(achieved / peak, 4),
             # the PMC profile is of one pipe.B-frame forward (its launches are the same per-slice
             # launches timed here), so it is looked up by the forward batch
-            "traffic": load_traffic(name, pipe.B, precision),
+            "traffic": load_traffic(name, pipe.B, precision, model),
             "launch_batch": bs,
             "kernel": f"{name}: {n} launches/forward, avg {ms / n:.4f} ms, avg {flops / n / 1e9:.2f} GFLOP/launch",
             "all_conv": {"launches": len(conv), "ms": round(all_ms, 3), "tflops": round(all_fl / all_ms / 1e9, 1)},
@@ -693,7 +694,7 @@ def main():
             return
 
     # roofline of the dominant kernel (separate pass with per-launch events)
-    roof = conv_roofline(pipe, frames, args.precision)
+    roof = conv_roofline(pipe, frames, args.precision, model=args.model)
     flops_frame = pipe.eng.geom["flops_per_frame"]
     extras = {}
     if rank == 0 and not args.no_extras:

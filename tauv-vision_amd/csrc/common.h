@@ -112,9 +112,11 @@ constexpr int kConv3MaxN = 2048;
 // 128-channel tensor summed into the same accumulators (ResidualBlock conv2 + conv_residual)
 // ni = 4: 128-channel tiles; ni = 2: 64-channel half tiles (epi 0 only; p.ntiles still counts
 // 128-channel tiles, the grid covers mtiles * ntiles * 2 work units)
+// nw = 8: one 512-thread workgroup per CU, 512-pixel tiles; nw = 4: two 256-thread workgroups per
+// CU, 256-pixel tiles (epi 0, res 0, 128-channel inputs, <= 256 output channels)
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s, int epi = 0, int res = 0, int ni = 4);
-int conv3x3_tiles(int B, int H, int W, int tw);
+                   hipStream_t s, int epi = 0, int res = 0, int ni = 4, int nw = 8);
+int conv3x3_tiles(int B, int H, int W, int tw, int nw = 8);
 // Persistent halo-tile 3x3 / stride 2 / pad 1 kernel (conv3x3s2.hip), fp16/bf16, 128 -> 128
 // channels: 16x32-pixel output tiles; ConvParams.mtiles = conv3x3s2_tiles(B, Ho, Wo), ntiles = 1
 int conv3x3s2_tiles(int B, int Ho, int Wo);
@@ -126,7 +128,7 @@ int launch_conv3x3s2(const ConvParams& p, const ConvParams* dp, void* out, int d
 size_t conv3x3_weight_bytes(int ntiles, int res, int ncb);
 int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, int k16, void* out, hipStream_t s);
 // whether the conv3x3 instance (epi, res, ni) runs the 16x16x32 body (its weights use that body's swizzle)
-int conv3x3_k16(int epi, int res, int ni);
+int conv3x3_k16(int epi, int res, int ni, int nw);
 
 // p: host copy (grid geometry); dp: the same struct in device memory; out: output base.
 int launch_conv(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,

@@ -24,8 +24,8 @@ __global__ void repack_weights(const uint4* __restrict__ w, int kpad16, int ntil
 
 }  // namespace c3
 
-int conv3x3_tiles(int B, int H, int W, int tw) {
-  const int th = c3::P / tw;
+int conv3x3_tiles(int B, int H, int W, int tw, int nw) {
+  const int th = 64 * nw / tw;
   return B * ((H + th - 1) / th) * ((W + tw - 1) / tw);
 }
 
@@ -33,7 +33,7 @@ size_t conv3x3_weight_bytes(int ntiles, int res, int ncb) {
   return (size_t)ntiles * (9 + res) * ncb * c3::WSLOT;
 }
 
-int conv3x3_k16(int epi, int res, int ni) { return c3::M16 && !res && epi == 0 && ni == 4; }
+int conv3x3_k16(int epi, int res, int ni, int nw) { return c3::M16 && !res && epi == 0 && ni == 4 && nw == 8; }
 
 int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni, int ncb, int k16, void* out, hipStream_t s) {
   if ((Kpad * esz) % 16 || Kpad < (9 * ncb + res) * 32 || (ni != 4 && ni != 2) || (ncb != 2 && ncb != 4 && ncb != 8)) {
@@ -47,7 +47,7 @@ int conv3x3_repack(const void* w, int Kpad, int esz, int ntiles, int res, int ni
 }
 
 int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid,
-                   hipStream_t s, int epi, int res, int ni) {
+                   hipStream_t s, int epi, int res, int ni, int nw) {
   using namespace c3;
   if (p.act < 0 || p.act > 2 || (ni != 4 && ni != 2) || (ni == 2 && epi != 0)) {
     set_error("conv3x3: bad activation / channel tile");
@@ -58,9 +58,13 @@ int launch_conv3x3(const ConvParams& p, const ConvParams* dp, void* out, int dty
     set_error("conv3x3: inputs of 64, 128 or 256 channels");
     return 1;
   }
-  if (ncb == 2) return launch_ncb2(p, dp, out, dtype, tw, grid, s, epi, res, ni);
-  if (ncb == 8) return launch_ncb8(p, dp, out, dtype, tw, grid, s, epi, res, ni);
-  return launch_ncb4(p, dp, out, dtype, tw, grid, s, epi, res, ni);
+  if (nw != 8 && (nw != 4 || epi || res)) {
+    set_error("conv3x3: 8-wave workgroups, or 4-wave ones with the plain epilogue");
+    return 1;
+  }
+  if (ncb == 2) return launch_ncb2(p, dp, out, dtype, tw, grid, s, epi, res, ni, nw);
+  if (ncb == 8) return launch_ncb8(p, dp, out, dtype, tw, grid, s, epi, res, ni, nw);
+  return launch_ncb4(p, dp, out, dtype, tw, grid, s, epi, res, ni, nw);
 }
 
 }  // namespace tv

@@ -155,6 +155,32 @@ static_assert(lds_bytes<1>() <= 160 * 1024 && lds_bytes<0, 1>() <= 160 * 1024, "
 static_assert(WSLOT / 1024 == NW, "one weight piece per wave per k-step");
 static_assert(HPIECES * 64 >= HPIX * 5, "halo pieces");
 
+// Tile geometry per workgroup size: NWV = 8 waves (one 512-thread workgroup per CU, the constants
+// above) or 4 (two independent 256-thread workgroups per CU, 256-pixel tiles: while one
+// workgroup waits at its per-k-step barrier or streams its epilogue stores, the other's waves keep
+// the same SIMDs' matrix cores busy; plain epilogue only, <= 256 output channels, 80 KiB of LDS).
+template <int NWV, int TW>
+struct Geo {
+  static constexpr int NW = NWV, NT = 64 * NWV, P = 64 * NWV, TH = P / TW, RS = TW + 2;
+  static constexpr int HPIX = (TH + 2) * RS;
+  static constexpr int HPIECES = (HPIX * 5 + 63) / 64;         // LDS-DMA pieces of 1 KiB per halo
+  static constexpr int HPW = (HPIECES + NW - 1) / NW;          // halo pieces per wave per channel block
+  static constexpr int HBUF = HPIECES * 1024;
+  static constexpr bool SINK = HPW * NW > HPIECES;             // surplus pieces (all lanes OOB) land here
+  static constexpr int OFF_D = 2 * HBUF;
+  static constexpr int OFF_W = 2 * HBUF + (SINK ? 1024 : 0);
+  static constexpr int OFF_B = OFF_W + RING * WSLOT;
+  static constexpr int MAXN = NWV == 8 ? kConv3MaxN : 256;     // bias entries in LDS
+  static constexpr int OFF_R = OFF_B + MAXN * 4;
+  static constexpr int RPW = RBUF / 1024 / NW;
+  static constexpr int OFF_HW = OFF_R, OFF_HS = OFF_HW + 2 * HWB;
+  template <int RES, int EPI>
+  static constexpr int lds() { return OFF_R + (RES ? RBUF : EPI ? 2 * HWB + NW * HSW : 0); }
+};
+static_assert(Geo<8, 32>::OFF_W == OFF_W && Geo<8, 16>::HPIX == HPIX && Geo<8, 32>::HPW == HPW, "8-wave geometry");
+static_assert(Geo<4, 32>::lds<0, 0>() <= 80 * 1024 && Geo<4, 16>::lds<0, 0>() <= 80 * 1024, "two 4-wave workgroups per CU");
+
+
 typedef __attribute__((address_space(3))) char lds_char;
 typedef const __attribute__((address_space(1))) void gvoid;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -189,7 +215,10 @@ __device__ __forceinline__ void wait_vm_n(int n) {
     case 2: wait_vm<2>(); break;
     case 3: wait_vm<3>(); break;
     case 4: wait_vm<4>(); break;
-    default: wait_vm<5>(); break;
+    case 5: wait_vm<5>(); break;
+    case 6: wait_vm<6>(); break;
+    case 7: wait_vm<7>(); break;
+    default: wait_vm<8>(); break;
   }
 }
 
@@ -222,22 +251,32 @@ __device__ __forceinline__ void store_out(T* dst, const float (&v)[2][4], int lh
 
 // NI: 32-channel fragments per wave — 4 (a 128-channel tile) or 2 (a 64-channel half tile, twice
 // the work units for layers whose 128-channel tiles leave the last round of CUs mostly idle)
-template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI, int NCB>
-__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv3x3(
+template <typename T, typename OutT, int TW, int ACT, int EPI, int RES, int NI, int NCB, int NWV = 8>
+__global__ __attribute__((amdgpu_flat_work_group_size(64 * NWV, 64 * NWV), amdgpu_waves_per_eu(2, 2))) void conv3x3(
     const ConvParams* __restrict__ pp, void* out_ptr) {
+  constexpr int RG = RING, WD = 2;  // weight ring slots; k-steps between a slot's ds_write and its first use
+  using Gm = Geo<NWV, TW>;
+  constexpr int NW = Gm::NW, NT = Gm::NT, P = Gm::P, HPIX = Gm::HPIX, HPW = Gm::HPW, HTAPS = Gm::HPW, HBUF = Gm::HBUF;
+  constexpr int HPIECES = Gm::HPIECES, OFF_W = Gm::OFF_W, OFF_B = Gm::OFF_B, OFF_R = Gm::OFF_R, RPW = Gm::RPW;
+  constexpr int OFF_HW = Gm::OFF_HW, OFF_HS = Gm::OFF_HS;
+  static_assert(NWV == 8 || (NWV == 4 && !RES && EPI == 0), "4-wave workgroups: plain epilogue only");
   // The 16x16x32 body for the plain 128-channel-tile instances only. Measured (profiles/r3b): the
   // dominant 120x160 layer 1.476 -> 1.423 ms per slice; the fused-heads epilogue on 16x16 tiles
   // (16-pixel fragments, twice the head MFMAs' issue slots per pixel) 0.883 -> 0.950 ms; the
   // half-tile (NI 2) instances +1-3%; the residual instances need ~12 VGPRs more than the 256 of
   // two waves per SIMD.
-  constexpr bool K16 = M16 && !RES && EPI == 0 && NI == 4;
+  constexpr bool K16 = M16 && !RES && EPI == 0 && NI == 4 && NWV == 8;
   static_assert(NI == 4 || (NI == 2 && EPI == 0), "half tiles: plain epilogue only");
   static_assert(!(EPI == 1 && RES), "fused heads use the residual LDS region for their 1x1 weights");
   constexpr int SPTK = spt<RES, NCB>();  // k-steps per tile
   constexpr int BNK = 32 * NI;      // output channels per tile
   constexpr int WSL = BNK * 64;     // weight bytes per k-step (an LDS ring slot holds up to WSLOT)
-  constexpr int WPL = WSL / 512;    // weight bytes per lane per k-step (16 or 8)
-  using WReg = typename std::conditional<NI == 4, u32x4, u32x2>::type;
+  constexpr int WPL = WSL / NT;     // weight bytes per lane per k-step (8, 16 or 32)
+  constexpr int WLN = WPL == 32 ? 2 : 1;  // weight load instructions per lane per k-step
+  struct W32 {
+    u32x4 a, b;
+  };
+  using WReg = typename std::conditional<WPL == 32, W32, typename std::conditional<WPL == 16, u32x4, u32x2>::type>::type;
   constexpr int TH = P / TW;
   constexpr int RS = TW + 2;                               // halo row stride (pixels)
   constexpr int FOFF = (TW == 32 ? 1 : 2) * RS * PITCH;    // next 32-pixel fragment
@@ -316,7 +355,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     wrsrc.z = ntiles * SPTK * WSL;
     wrsrc.w = 0x00020000;
   }
-  const int wvoff = wave * (WSL / 8) + lane * WPL;
+  const int wvoff = wave * (WSL / NW) + lane * WPL;
 
   // ---- tile decode
   auto tile_of = [&](int idx, int& fr, int& y0, int& x0, int& nt) __attribute__((always_inline)) {
@@ -356,7 +395,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // one halo piece (index I of this wave's HPW) of channel block cb into buffer bsel
   auto halo_piece = [&](auto pc, int cb, int bsel) __attribute__((always_inline)) {
     constexpr int I = decltype(pc)::value;
-    lds_char* base = lds + bsel * HBUF + (wave * HPW + I) * 1024;
+    // (a surplus piece past the halo's last — 4-wave workgroups — reads OOB zeros into the sink)
+    lds_char* base = !Gm::SINK || wave * HPW + I < HPIECES ? lds + bsel * HBUF + (wave * HPW + I) * 1024 : lds + Gm::OFF_D;
     raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)base, 16, (int)hoff[I],
                         cb * CBK * (int)sizeof(T), 0, 0);
   };
@@ -413,8 +453,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // ring slot with ds_write_b128 one step later (instead of an LDS-DMA piece per k-step)
   WReg wreg[4];  // k-step q's weights are loaded at step q-5 into set q % 4
   auto w_load = [&](WReg& dst) __attribute__((always_inline)) {
-    if constexpr (NI == 4) dst = raw_buffer_load_v4(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
-    else dst = raw_buffer_load_v2(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
+    if constexpr (WPL == 32) {
+      dst.a = raw_buffer_load_v4(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
+      dst.b = raw_buffer_load_v4(wrsrc, wvoff + 16, (wc_nt * SPTK + wc_in) * WSL, 0);
+    } else if constexpr (WPL == 16) {
+      dst = raw_buffer_load_v4(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
+    } else {
+      dst = raw_buffer_load_v2(wrsrc, wvoff, (wc_nt * SPTK + wc_in) * WSL, 0);
+    }
     if (++wc_in == SPTK) {
       wc_in = 0;
       if (++wc_idx < ntl) {
@@ -704,12 +750,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   int cur_fr, cur_y0, cur_x0, cur_nt;
   tile_of(0, cur_fr, cur_y0, cur_x0, cur_nt);
   halo_offsets(cur_fr, cur_y0, cur_x0);
-  halo_piece(IC<0>{}, 0, 0);
-  halo_piece(IC<1>{}, 0, 0);
-  halo_piece(IC<2>{}, 0, 0);
-  halo_piece(IC<3>{}, 0, 0);
-  halo_piece(IC<4>{}, 0, 0);
-  halo_piece(IC<5>{}, 0, 0);
+  auto halo_all = [&](auto self, auto i) __attribute__((always_inline)) {
+    constexpr int I = decltype(i)::value;
+    if constexpr (I < HPW) {
+      halo_piece(IC<I>{}, 0, 0);
+      self(self, IC<I + 1>{});
+    }
+  };
+  halo_all(halo_all, IC<0>{});
   __builtin_amdgcn_sched_barrier(0);  // the counted wait below needs the halo issued first
   // weights: k-steps 0, 1 into ring slots 0, 1; k-steps 2, 3, 4 in flight in sets 2, 3, 0
   // (S_tot >= SPTK > 5). Every VMEM operation of the main loop is issued unconditionally —
@@ -739,7 +787,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     __builtin_amdgcn_sched_barrier(0);
   }
   // the halo (issued first) landed; the weights of k-steps 2..4 (and the dropped stores) may stay in flight
-  wait_vm<EPI == 0 ? 3 + 4 * NI : 3>();
+  wait_vm<3 * WLN + (EPI == 0 ? 4 * NI : 0)>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -767,7 +815,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // static priority for the second-dispatched half (waves 4-7, the SIMD partners of waves 0-3):
   // the arbitration loser on every segment otherwise (MI355X_MICROARCH.md, two waves per SIMD,
   // item 4). Measured: 60x80 layers -3%, the others -0.4..-1%
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
   int s = 0;   // global k-step
   int tl = 0;  // tile index within this block's list
   int cb = 0;  // channel block within the tile (compile-time inside cblock)
@@ -790,13 +838,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     //    block's halo (last piece at tap 5): younger = the weight loads of taps 5, 6, 7 (and 8);
     //  * tap 8 with RES: the residual step reads this block's residual input (last piece at
     //    tap 4): younger = weight loads of taps 4, 5, 6, 7 + the tap-5 halo piece.
-    static_assert(HTAPS <= 6, "weight loads issued after the last halo piece must cover the tap-8 count");
+    static_assert(HTAPS == 6 || (HTAPS == 7 && !RES), "the tap-8 count: the last halo piece at tap 5 or 6");
     C3_STAMP(2);
 #if TV_C3_EXP == 9
     st_b[5] += 1;
 #endif
-    auto wl = [&](int q) { return q >= 0 ? 1 : 0; };
-    if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
+    auto wl = [&](int q) { return q >= 0 ? WLN : 0; };
+    // (the last halo piece goes out at tap HTAPS - 1: taps 5 or 6; the weight loads of the taps
+    // from there to 7 are younger)
+    if constexpr (TAP == 8 && !RES) wait_vm_n(s + 1 < S_tot ? (HTAPS <= 6 ? wl(s - 3) : 0) + wl(s - 2) + wl(s - 1) : 0);
     if constexpr (TAP == 8 && RES) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) + 1 : 0);
     if constexpr (TAP == 9) wait_vm_n(s + 1 < S_tot ? wl(s - 4) + wl(s - 3) + wl(s - 2) + wl(s - 1) : 0);
     if constexpr (TAP >= 8) C3_STAMP(6);
@@ -814,8 +864,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const int hbuf = (cb + 1) & 1;
     const unsigned xc = xa + (cb & 1) * HBUF;                                  // this k-step's halo
     const unsigned xn = xa + (NTAP == 0 ? hbuf : (cb & 1)) * HBUF;             // next k-step's halo
-    const unsigned wc1 = wa[1] + (unsigned)((s % RING) * WSLOT);
-    const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RING) * WSLOT);
+    const unsigned wc1 = wa[1] + (unsigned)((s % RG) * WSLOT);
+    const unsigned wn0 = wa[0] + (unsigned)(((s + 1) % RG) * WSLOT);
     // first half: sub-step 0 MFMAs; sub-step 1 reads of this k-step go out first (H1 is free)
     constexpr bool FIRST = TAP == 0 && decltype(first)::value;
     constexpr int PAR = decltype(par)::value;  // s % 4 (36 or 40 k-steps per tile: static)
@@ -827,8 +877,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       // (one operand set live: 4 + 2 NI fragments, as the 32x32 body's two sub-step sets); the
       // next k-step's channel fragments 0..NI-1 go into W16[0], free since the first half.
       const unsigned x16n = xa16 + (NTAP == 0 ? hbuf : (cb & 1)) * HBUF;
-      const unsigned w16c = wa16 + (unsigned)((s % RING) * WSLOT);
-      const unsigned w16n = wa16 + (unsigned)(((s + 1) % RING) * WSLOT);
+      const unsigned w16c = wa16 + (unsigned)((s % RG) * WSLOT);
+      const unsigned w16n = wa16 + (unsigned)(((s + 1) % RG) * WSLOT);
       u32x4(&X)[4] = X16[0];
       u32x4(&WA)[NI] = W16[0];
       u32x4(&WB)[NI] = W16[1];
@@ -842,7 +892,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         WB[3] = ds_read16<7 * 1024>(w16c);
       }
 #if TV_C3_EXP != 6
-      *reinterpret_cast<WReg*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wvoff) = wreg[(PAR + 2) & 3];
+      *reinterpret_cast<WReg*>(smem + OFF_W + ((s + WD) % RG) * WSLOT + wvoff) = wreg[(PAR + WD) & 3];
 #endif
       if constexpr (TAP == 0) {
         if (nxt_exists && nxt_newtile) {
@@ -902,7 +952,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // k-step s+2 (loaded at step s-3) into its ring slot: it last held k-step s-1, read
     // completely before this step's barrier (past the end: an unread slot)
 #if TV_C3_EXP != 6  // 6: timing only, no weight ds_write (wrong results)
-    *reinterpret_cast<WReg*>(smem + OFF_W + ((s + 2) % RING) * WSLOT + wvoff) = wreg[(PAR + 2) & 3];
+    *reinterpret_cast<WReg*>(smem + OFF_W + ((s + WD) % RG) * WSLOT + wvoff) = wreg[(PAR + WD) & 3];
 #endif
     if constexpr (TAP == 0) {
       if (nxt_exists && nxt_newtile) {
@@ -1018,25 +1068,48 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 #endif
 }
 
-template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4, int NCB = 4>
+template <typename T, int TW, int ACT, int EPI = 0, int RES = 0, int NI = 4, int NCB = 4, int NWV = 8>
 inline int launch_t(const ConvParams& p, const ConvParams* dp, void* out, int grid, hipStream_t s) {
-  auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>;
-  constexpr int lds = lds_bytes<RES, EPI>();
-  if (int r = ensure_lds<conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB>>(lds)) return r;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, out);
+  auto k = conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB, NWV>;
+  using Gm = Geo<NWV, TW>;
+  constexpr int lds = Gm::template lds<RES, EPI>();
+  if (NWV == 4 && p.ntiles * BN > Gm::MAXN) {
+    set_error("conv3x3: 4-wave workgroups take <= 256 output channels");
+    return 1;
+  }
+  if (int r = ensure_lds<conv3x3<T, T, TW, ACT, EPI, RES, NI, NCB, NWV>>(lds)) return r;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * NWV), lds, s, dp, out);
   TV_HIP(hipGetLastError());
   return 0;
 }
 
 
 using Launch = int (*)(const ConvParams&, const ConvParams*, void*, int, hipStream_t);
+// the plain-epilogue instances of a channel-block count and workgroup size: [bf16][ni == 4][tw == 32][act]
+template <int NCB, int NWV>
+int launch_plain(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s, int ni) {
+  static const Launch t[2][2][2][3] = {
+      {{{launch_t<_Float16, 16, 0, 0, 0, 2, NCB, NWV>, launch_t<_Float16, 16, 1, 0, 0, 2, NCB, NWV>, launch_t<_Float16, 16, 2, 0, 0, 2, NCB, NWV>},
+        {launch_t<_Float16, 32, 0, 0, 0, 2, NCB, NWV>, launch_t<_Float16, 32, 1, 0, 0, 2, NCB, NWV>, launch_t<_Float16, 32, 2, 0, 0, 2, NCB, NWV>}},
+       {{launch_t<_Float16, 16, 0, 0, 0, 4, NCB, NWV>, launch_t<_Float16, 16, 1, 0, 0, 4, NCB, NWV>, launch_t<_Float16, 16, 2, 0, 0, 4, NCB, NWV>},
+        {launch_t<_Float16, 32, 0, 0, 0, 4, NCB, NWV>, launch_t<_Float16, 32, 1, 0, 0, 4, NCB, NWV>, launch_t<_Float16, 32, 2, 0, 0, 4, NCB, NWV>}}},
+      {{{launch_t<__bf16, 16, 0, 0, 0, 2, NCB, NWV>, launch_t<__bf16, 16, 1, 0, 0, 2, NCB, NWV>, launch_t<__bf16, 16, 2, 0, 0, 2, NCB, NWV>},
+        {launch_t<__bf16, 32, 0, 0, 0, 2, NCB, NWV>, launch_t<__bf16, 32, 1, 0, 0, 2, NCB, NWV>, launch_t<__bf16, 32, 2, 0, 0, 2, NCB, NWV>}},
+       {{launch_t<__bf16, 16, 0, 0, 0, 4, NCB, NWV>, launch_t<__bf16, 16, 1, 0, 0, 4, NCB, NWV>, launch_t<__bf16, 16, 2, 0, 0, 4, NCB, NWV>},
+        {launch_t<__bf16, 32, 0, 0, 0, 4, NCB, NWV>, launch_t<__bf16, 32, 1, 0, 0, 4, NCB, NWV>, launch_t<__bf16, 32, 2, 0, 0, 4, NCB, NWV>}}}};
+  if (dtype != F16 && dtype != BF16) {
+    set_error("conv3x3: fp16/bf16 only");
+    return 1;
+  }
+  return t[dtype == BF16][ni == 4][tw == 32][p.act](p, dp, out, grid, s);
+}
 // per input-channel-count instance tables (conv3x3_n2/n4/n8.hip)
 int launch_ncb2(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,
-                int epi, int res, int ni);
+                int epi, int res, int ni, int nw);
 int launch_ncb4(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,
-                int epi, int res, int ni);
+                int epi, int res, int ni, int nw);
 int launch_ncb8(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,
-                int epi, int res, int ni);
+                int epi, int res, int ni, int nw);
 // the residual (RES) instances of a channel-block count: ReLU, plain stores, [bf16][tw == 32][ni == 4]
 template <int NCB>
 int launch_res(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s,

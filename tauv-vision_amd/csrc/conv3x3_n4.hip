@@ -5,7 +5,7 @@ namespace tv {
 namespace c3 {
 
 int launch_ncb4(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s, int epi,
-                int res, int ni) {
+                int res, int ni, int nw) {
   if (res) return launch_res<4>(p, dp, out, dtype, tw, grid, s, epi, ni);  // ResidualBlock conv2 + conv_residual
   if (epi == 1) {  // fused 1x1 heads: the stacked heads' LeakyReLU only
     if (p.act != 2 || p.ntiles > 16) {
@@ -17,20 +17,8 @@ int launch_ncb4(const ConvParams& p, const ConvParams* dp, void* out, int dtype,
     set_error("conv3x3: fp16/bf16 only");
     return 1;
   }
-  static const Launch f16[2][2][3] = {
-      {{launch_t<_Float16, 16, 0, 0, 0, 2>, launch_t<_Float16, 16, 1, 0, 0, 2>, launch_t<_Float16, 16, 2, 0, 0, 2>},
-       {launch_t<_Float16, 32, 0, 0, 0, 2>, launch_t<_Float16, 32, 1, 0, 0, 2>, launch_t<_Float16, 32, 2, 0, 0, 2>}},
-      {{launch_t<_Float16, 16, 0>, launch_t<_Float16, 16, 1>, launch_t<_Float16, 16, 2>},
-       {launch_t<_Float16, 32, 0>, launch_t<_Float16, 32, 1>, launch_t<_Float16, 32, 2>}}};
-  static const Launch b16[2][2][3] = {
-      {{launch_t<__bf16, 16, 0, 0, 0, 2>, launch_t<__bf16, 16, 1, 0, 0, 2>, launch_t<__bf16, 16, 2, 0, 0, 2>},
-       {launch_t<__bf16, 32, 0, 0, 0, 2>, launch_t<__bf16, 32, 1, 0, 0, 2>, launch_t<__bf16, 32, 2, 0, 0, 2>}},
-      {{launch_t<__bf16, 16, 0>, launch_t<__bf16, 16, 1>, launch_t<__bf16, 16, 2>},
-       {launch_t<__bf16, 32, 0>, launch_t<__bf16, 32, 1>, launch_t<__bf16, 32, 2>}}};
-  if (dtype == F16) return f16[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-  if (dtype == BF16) return b16[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-  set_error("conv3x3: fp16/bf16 only");
-  return 1;
+  if (nw == 4) return launch_plain<4, 4>(p, dp, out, dtype, tw, grid, s, ni);
+  return launch_plain<4, 8>(p, dp, out, dtype, tw, grid, s, ni);
 
 }
 

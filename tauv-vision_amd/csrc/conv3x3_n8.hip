@@ -5,7 +5,7 @@ namespace tv {
 namespace c3 {
 
 int launch_ncb8(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int tw, int grid, hipStream_t s, int epi,
-                int res, int ni) {
+                int res, int ni, int nw) {
   if (res) return launch_res<8>(p, dp, out, dtype, tw, grid, s, epi, ni);  // DLA-34 BasicBlock identity residual
   // 256-channel inputs (protonet, DLA-34 level 4)
     if (epi == 1) {
@@ -18,20 +18,11 @@ int launch_ncb8(const ConvParams& p, const ConvParams* dp, void* out, int dtype,
       set_error("conv3x3: fp16/bf16 only");
       return 1;
     }
-    static const Launch f8[2][2][3] = {
-        {{launch_t<_Float16, 16, 0, 0, 0, 2, 8>, launch_t<_Float16, 16, 1, 0, 0, 2, 8>, launch_t<_Float16, 16, 2, 0, 0, 2, 8>},
-         {launch_t<_Float16, 32, 0, 0, 0, 2, 8>, launch_t<_Float16, 32, 1, 0, 0, 2, 8>, launch_t<_Float16, 32, 2, 0, 0, 2, 8>}},
-        {{launch_t<_Float16, 16, 0, 0, 0, 4, 8>, launch_t<_Float16, 16, 1, 0, 0, 4, 8>, launch_t<_Float16, 16, 2, 0, 0, 4, 8>},
-         {launch_t<_Float16, 32, 0, 0, 0, 4, 8>, launch_t<_Float16, 32, 1, 0, 0, 4, 8>, launch_t<_Float16, 32, 2, 0, 0, 4, 8>}}};
-    static const Launch b8[2][2][3] = {
-        {{launch_t<__bf16, 16, 0, 0, 0, 2, 8>, launch_t<__bf16, 16, 1, 0, 0, 2, 8>, launch_t<__bf16, 16, 2, 0, 0, 2, 8>},
-         {launch_t<__bf16, 32, 0, 0, 0, 2, 8>, launch_t<__bf16, 32, 1, 0, 0, 2, 8>, launch_t<__bf16, 32, 2, 0, 0, 2, 8>}},
-        {{launch_t<__bf16, 16, 0, 0, 0, 4, 8>, launch_t<__bf16, 16, 1, 0, 0, 4, 8>, launch_t<__bf16, 16, 2, 0, 0, 4, 8>},
-         {launch_t<__bf16, 32, 0, 0, 0, 4, 8>, launch_t<__bf16, 32, 1, 0, 0, 4, 8>, launch_t<__bf16, 32, 2, 0, 0, 4, 8>}}};
-    if (dtype == F16) return f8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-    if (dtype == BF16) return b8[ni == 4][tw == 32][p.act](p, dp, out, grid, s);
-    set_error("conv3x3: fp16/bf16 only");
+    if (nw != 8) {
+    set_error("conv3x3: 4-wave workgroups for 128-channel inputs only");
     return 1;
+  }
+  return launch_plain<8, 8>(p, dp, out, dtype, tw, grid, s, ni);
   
 }
 

@@ -99,8 +99,11 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int hw = p.h * p.w;
   const int M = p.B * hw;
   const int mt = (M + 31) / 32;
-  const int t_begin = (chunk * NW + wave) * p.tpw;
-  const int t_end = min(t_begin + p.tpw, mt);
+  // this wave's contiguous run of the group's tiles: an even split over all the group's waves
+  // (every CU busy: the pass is bound by each CU's own ~10 B/clk of HBM loads)
+  const long long gw = (long long)chunk * NW + wave, nw = (long long)p.nchunks * NW;
+  const int t_begin = (int)(mt * gw / nw);
+  const int t_end = (int)(mt * (gw + 1) / nw);
   if (t_begin >= t_end) return;
 
   // target element offset (channel 0) of this lane's pixel in tile t for phase ph, or -1
@@ -249,7 +252,9 @@ bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc) {
   return cin == convt::KJ * 16 && cout == convt::C && src_ldc % 8 == 0 && add_ldc % 8 == 0 && out_ldc % 8 == 0;
 }
 
-// tiles per wave: about one resident 8-wave workgroup per CU over the whole launch, >= 2 tiles per wave
+// one resident 8-wave workgroup per CU over the whole launch, the tiles split evenly over the
+// waves of each phase group (round-2 schedule: whole tiles-per-wave counts, which left 56 of 256
+// CUs idle on the 120x160 up-steps)
 void convt_schedule(ConvTParams& p, int cu_count) {
   const long M = (long)p.B * p.h * p.w;
   const long mt = (M + 31) / 32;
@@ -258,11 +263,12 @@ void convt_schedule(ConvTParams& p, int cu_count) {
   p.np = (p.s * p.s % convt::NPG == 0 &&
           mt * (p.s * p.s / convt::NPG) >= 2 * waves_target) ? convt::NPG : 1;
   const long groups = (long)p.s * p.s / p.np;
-  long per_group = (waves_target + groups - 1) / groups;
-  long tpw = (mt + per_group - 1) / per_group;
-  if (tpw < 1) tpw = 1;
-  p.tpw = (int)tpw;
-  p.nchunks = (int)((mt + convt::NW * tpw - 1) / (convt::NW * tpw));
+  long chunks = cu_count / groups;                       // workgroups per phase group
+  const long need = (mt + convt::NW - 1) / convt::NW;    // no more than one tile per wave's worth
+  if (chunks > need) chunks = need;
+  if (chunks < 1) chunks = 1;
+  p.nchunks = (int)chunks;
+  p.tpw = (int)((mt + chunks * convt::NW - 1) / (chunks * convt::NW));  // most tiles any wave runs
 }
 
 int launch_convt(const ConvTParams& p, int dtype, hipStream_t s) {

@@ -312,6 +312,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_HEADFUSE") headfuse_mode = v;
     else if (k == "TV_S2_MINTILES") s2_min_tiles = v;
     else if (k == "TV_C3_NI") c3_ni_force = v == 2 ? 2 : v == 4 ? 4 : 0;
+    else if (k == "TV_C3_NW") c3_nw_mode = v == 8 ? 8 : 0;
     else if (k == "TV_C3_HALF_COST") c3_half_cost = v;
     else if (k == "TV_SLICES") slices = std::max(1, std::min(kMaxSlices, v));
     else if (k == "TV_C3_STAMPS") {  // "op:device pointer" (stamp builds of conv3x3 only)
@@ -517,6 +518,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   ws->s2_grid.assign(plan.ops.size(), 0);
   ws->c3_res.assign(plan.ops.size(), 0);
   ws->c3_ni.assign(plan.ops.size(), 4);
+  ws->c3_nw.assign(plan.ops.size(), 8);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (op.kind != OP_CONV && op.kind != OP_CONVT_ADD) continue;
@@ -582,34 +584,52 @@ int Engine::make_workspace(int B, Workspace* ws) {
           p.ntiles * 128 <= kConv3MaxN && p.act >= 0 && p.act <= 2 && cs.H * cs.W >= conv3_min_pix &&
           (size_t)cs.H * cs.W * p.out_ldc * esz < (1ull << 31)) {
         const int res = res2 ? 1 : 0;
-        const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16), t32 = conv3x3_tiles(B, cs.H, cs.W, 32);
-        const int tw = c3_tw_force ? c3_tw_force : t32 <= t16 ? 32 : 16;
-        const int mt = tw == 32 ? t32 : t16;
-        // 64-channel half tiles when the last round of 128-channel tiles would leave most CUs
-        // idle: a half tile costs ~c3_half_cost of a full one (two work units per tile)
-        const long t4 = (long)mt * p.ntiles;
-        const long r4 = (t4 + cu_count - 1) / cu_count, r2 = (2 * t4 + cu_count - 1) / cu_count;
-        int ni = c3_ni_force ? c3_ni_force : (c3_half_cost > 0 && c3_half_cost * r2 < 100 * r4) ? 2 : 4;
-        if (p.N <= 64) ni = 2;  // one 64-channel half tile holds every output channel
-        if (op.act >= 1 && !res && op.out >= 0 && i + 1 < plan.ops.size() && !plan.ops[i + 1].diag_in_off.empty())
-          ni = 4;  // the stacked heads (fused 1x1 epilogue) keep 128-channel tiles
+        const bool heads = op.act >= 1 && !res && op.out >= 0 && i + 1 < plan.ops.size() &&
+                           !plan.ops[i + 1].diag_in_off.empty();
+        int nw = 8, tw = 0, mt = 0, ni = 4;
+        long t4 = 0;
+        auto geometry = [&](int nwv) {  // tile width, tiles and channel-tile choice for a workgroup size
+          const int slots = nwv == 4 ? 2 * cu_count : cu_count;  // resident workgroups
+          const int t16 = conv3x3_tiles(B, cs.H, cs.W, 16, nwv), t32 = conv3x3_tiles(B, cs.H, cs.W, 32, nwv);
+          tw = c3_tw_force ? c3_tw_force : t32 <= t16 ? 32 : 16;
+          mt = tw == 32 ? t32 : t16;
+          // 64-channel half tiles when the last round of 128-channel tiles would leave most CUs
+          // idle: a half tile costs ~c3_half_cost of a full one (two work units per tile)
+          t4 = (long)mt * p.ntiles;
+          const long r4 = (t4 + slots - 1) / slots, r2 = (2 * t4 + slots - 1) / slots;
+          ni = c3_ni_force ? c3_ni_force : (c3_half_cost > 0 && c3_half_cost * r2 < 100 * r4) ? 2 : 4;
+          if (p.N <= 64) ni = 2;  // one 64-channel half tile holds every output channel
+          if (heads) ni = 4;      // the stacked heads (fused 1x1 epilogue) keep 128-channel tiles
+        };
+        geometry(8);
+        // two 4-wave workgroups per CU (256-pixel tiles) for the plain 128-channel-input convs that
+        // run 64-channel half tiles. Measured (profiles/r3c): the R18 60x80 layers 1.000 -> 0.916 ms
+        // per slice; on the dominant 120x160 layer (128-channel tiles) 1.432 -> 1.506 ms, so those
+        // keep one 8-wave workgroup per CU
+        if (ni == 2 && c3_nw_mode != 8 && !res && !heads && cs.C == 128 && p.ntiles <= 2) {
+          nw = 4;
+          geometry(4);
+          ni = 2;
+        }
+        const int slots = nw == 4 ? 2 * cu_count : cu_count;
         const long total = (ni == 2 && p.N <= 64) ? t4 : t4 * (4 / ni);
-        int grid = (int)std::min<long>(total, cu_count);
+        int grid = (int)std::min<long>(total, slots);
         // XCD-aware contiguous ranges need a multiple of 8 workgroups; rounding down is only
         // worth it when every workgroup still gets several units (measured at B=1: 20 units on
         // 16 workgroups ran two rounds, 29 us instead of 18)
-        if (grid >= 8 && total > 2L * cu_count) grid -= grid % 8;
+        if (grid >= 8 && total > 2L * slots) grid -= grid % 8;
         Packed& pk3 = packed[i];
         void*& wc = ni == 4 ? pk3.w_c3 : pk3.w_c3h;
         if (!wc) {
           TV_HIP(hipMalloc(&wc, conv3x3_weight_bytes(p.ntiles, res, cs.C / 32)));
-          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, ni, cs.C / 32, conv3x3_k16(0, res, ni), wc, nullptr);
+          int rc = conv3x3_repack(pk3.w, pk3.Kpad, esz, p.ntiles, res, ni, cs.C / 32, conv3x3_k16(0, res, ni, nw), wc, nullptr);
           if (rc) return rc;
           TV_HIP(hipDeviceSynchronize());
         }
         p.weight = wc;
         ws->c3_tw[i] = tw;
         ws->c3_ni[i] = ni;
+        ws->c3_nw[i] = nw;
         ws->c3_res[i] = res;
         ws->c3_grid[i] = grid;
         ws->use_pipe[i] = 0;
@@ -693,17 +713,17 @@ int Engine::make_workspace(int B, Workspace* ws) {
   for (size_t i = 0; headfuse_mode && i + 1 < plan.ops.size(); ++i) {
     const OpSpec& h2 = plan.ops[i + 1];
     const Packed& pk2 = packed[i + 1];
-    if (!ws->c3_tw[i] || ws->c3_ni[i] != 4 || h2.diag_in_off.empty() || !pk2.head_ok || h2.out >= 0 || h2.segs[0].src != plan.ops[i].out ||
+    if (!ws->c3_tw[i] || ws->c3_ni[i] != 4 || ws->c3_nw[i] != 8 || h2.diag_in_off.empty() || !pk2.head_ok || h2.out >= 0 || h2.segs[0].src != plan.ops[i].out ||
         (plan.ops[i].act != 2 && !(plan.ops[i].act == 1 && plan.tensors[plan.ops[i].segs[0].src].C == 64)) ||
         ws->params[i].ntiles != plan.ops[i].N / 128)
       continue;
     ConvParams& p = ws->params[i];
-    if (conv3x3_k16(1, 0, 4) != conv3x3_k16(0, 0, 4)) {  // the fused-heads body reads the other swizzle
+    if (conv3x3_k16(1, 0, 4, 8) != conv3x3_k16(0, 0, 4, 8)) {  // the fused-heads body reads the other swizzle
       Packed& pk3 = packed[i];
       if (!pk3.w_c3e) {
         const int ncb = plan.tensors[plan.ops[i].segs[0].src].C / 32;
         TV_HIP(hipMalloc(&pk3.w_c3e, conv3x3_weight_bytes(p.ntiles, 0, ncb)));
-        int rc = conv3x3_repack(pk3.w, pk3.Kpad, dtype_size(dtype), p.ntiles, 0, 4, ncb, conv3x3_k16(1, 0, 4), pk3.w_c3e, nullptr);
+        int rc = conv3x3_repack(pk3.w, pk3.Kpad, dtype_size(dtype), p.ntiles, 0, 4, ncb, conv3x3_k16(1, 0, 4, 8), pk3.w_c3e, nullptr);
         if (rc) return rc;
         TV_HIP(hipDeviceSynchronize());
       }
@@ -763,7 +783,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
         p.out_ldc % 8 || p.out_coff % 8)
       continue;
     long units;
-    if (ws->c3_tw[i]) units = (long)p.mtiles * p.ntiles * (ws->c3_ni[i] == 2 && p.N > 64 ? 2 : 1);
+    if (ws->c3_tw[i]) units = (long)p.mtiles * p.ntiles * (ws->c3_ni[i] == 2 && p.N > 64 ? 2 : 1) / (ws->c3_nw[i] == 4 ? 2 : 1);
     else if (ws->s2_grid[i]) units = p.mtiles;
     else if (ws->use_pipe[i]) units = (long)p.mtiles * p.ntiles;
     else units = 0;  // conv_igemm corner case: always worse than conv_lat
@@ -906,7 +926,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   if (ws->lat[i]) return launch_conv_lat(p, ws->dparams + i, dtype, s);
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
-                                           ws->c3_res[i], ws->c3_ni[i])
+                                           ws->c3_res[i], ws->c3_ni[i], ws->c3_nw[i])
            : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
                              : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
   if (rc) return rc;
@@ -1052,7 +1072,7 @@ const char* Engine::op_kernel(int B, size_t i) {
       else if (ws->lat[i])
         name = std::string("tv::lat::conv_lat<") + t + ">";
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
-      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ">";
+      else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ", " + std::to_string(ws->c3_nw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";
     }

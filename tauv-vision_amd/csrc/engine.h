@@ -38,6 +38,7 @@ struct Workspace {
   std::vector<int> c3_tw, c3_grid;  // per op: > 0 = persistent conv3x3 (tile width, workgroups); overrides all
   std::vector<int> c3_res;          // per op: 1 = conv3x3 with the 1x1 residual segment (RES)
   std::vector<int> c3_ni;           // per op: channel fragments per wave (4: 128-channel tiles, 2: 64)
+  std::vector<int> c3_nw;           // per op: waves per workgroup (8: one per CU, 4: two per CU)
   std::vector<int> s2_grid;         // per op: > 0 = persistent stride-2 conv3x3s2 (workgroups)
   std::vector<int> head_fused;      // per op: 1 = stacked 3x3 heads with the 1x1 heads fused in
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
@@ -64,6 +65,7 @@ struct Engine {
   int s2_min_tiles = 1;        // stride-2 halo kernel from this many tiles (env TV_S2_MINTILES; -1 = cu_count; measured:
                                // at B=1 the halo kernel beats the implicit GEMM on the small levels too)
   int c3_ni_force = 0;         // conv3x3 channel tile: 0 = by grid rounds, 2 / 4 forced (env TV_C3_NI)
+  int c3_nw_mode = 0;          // conv3x3 workgroup size: 0 = 4-wave where eligible, 8 = always 8 (TV_C3_NW)
   int c3_half_cost = 55;       // cost of a 64-channel half tile in % of a full one (env TV_C3_HALF_COST, 0 = never)
   int conv3_min_pix = 1;       // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)
   int s2_mode = 1;             // stride-2 halo kernel for eligible fp16/bf16 layers (env TV_CONV3S2=0 off)

@@ -276,6 +276,10 @@ def parity_leg(model, oc, mc, arch, B, K, device):
             res[k] = max(res[k], pp[k])
         res["heatmap_drift"] = max(res["heatmap_drift"], drift)
     res = {k: (round(v, 7) if isinstance(v, float) else v) for k, v in res.items()}
+    # which bar the timed precision meets: the north star's "detections within 1e-4 of reference"
+    # is an fp32 statement; the fp32 path meets it (fp32_value; tests/test_gpu_forward.py), the
+    # fp16 / bf16 paths are held to detection-level parity (tests/test_gpu_parity_lowp.py)
+    res["within_1e-4"] = bool(res["agreement"] == 1.0 and res["max_box_err"] <= 1e-4 and res["max_score_err"] <= 1e-4)
     res.update({"K": K, "frames_checked": len(slots), "batch": B,
                 "reference": f"tests/golden/{name}.npz (reference decode K=100 records)"})
     return res

@@ -9,8 +9,12 @@
 //
 // fast_nms, any anchor count, B images per launch (the reference runs image 0 only: :14,25):
 //   nms_keys    one thread per anchor: the confidence as an order-preserving 32-bit key;
-//   sort        rocPRIM segmented radix sort (one segment per image, descending, stable: equal
-//               confidences keep ascending anchor order), values = anchor ids;
+//   nms_topk    one 1024-thread workgroup per image (top_k <= 1024, anchors <= 32768): the
+//               anchors' 64-bit keys (confidence key << 32 | ~anchor: unique, descending order
+//               = the reference's stable descending sort, equal confidences in ascending anchor
+//               order) in registers, the K-th largest found by 8 radix passes of 8-bit digits
+//               over LDS histograms, the K keys >= it compacted into LDS and bitonic-sorted;
+//               larger top_k / anchor counts take a rocPRIM segmented radix sort (the same order);
 //   nms_iou     one thread per kept column j < min(top_k, A); rows i < j staged through LDS in
 //               256-box chunks; the column max propagates NaN like torch.max (0/0 IoUs of two
 //               zero-area boxes drop the column: NaN <= thr is false);
@@ -169,6 +173,93 @@ __global__ __launch_bounds__(kCompactThreads) void nms_compact(const uint8_t* __
   }
   __syncthreads();
   if (tid == 0) n_det[b] = base;
+}
+
+// ---- exact per-image top-K of the NMS keys (nms_topk) ---------------------------------------
+constexpr int kTopkThreads = 1024;
+constexpr int kTopkMaxK = 1024;
+template <int PER>  // keys per thread: A <= PER * 1024
+__global__ __launch_bounds__(kTopkThreads) void nms_topk(const uint32_t* __restrict__ keys, int A, int K,
+                                                         uint32_t* __restrict__ skeys, int* __restrict__ sidx) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned long long sel[kTopkMaxK];
+  __shared__ unsigned s_digit, s_above, s_n;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t seg = (size_t)b * A;
+  unsigned long long k[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int a = tid + j * kTopkThreads;
+    // key 0 never occurs for a real anchor: its low word ~a is nonzero for a < 2^32 - 1
+    k[j] = a < A ? ((unsigned long long)keys[seg + a] << 32) | (0xFFFFFFFFu - (unsigned)a) : 0ull;
+  }
+  // radix select of the K-th largest key, most significant digit first
+  unsigned long long prefix = 0, pmask = 0;
+  unsigned need = (unsigned)K;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    if (tid < 256) hist[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (k[j] != 0 && (k[j] & pmask) == prefix) atomicAdd(&hist[(unsigned)(k[j] >> shift) & 255u], 1u);
+    __syncthreads();
+    if (tid < 64) {  // one wave: the digit whose suffix count first reaches `need`
+      const unsigned h0 = hist[255 - 4 * tid], h1 = hist[254 - 4 * tid], h2 = hist[253 - 4 * tid], h3 = hist[252 - 4 * tid];
+      const unsigned own = h0 + h1 + h2 + h3;
+      unsigned incl = own;  // inclusive prefix over lanes (digits descending)
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(incl, d, 64);
+        if (tid >= d) incl += o;
+      }
+      const unsigned excl = incl - own;
+      if (excl < need && incl >= need) {
+        unsigned above = excl;
+        const unsigned hs[4] = {h0, h1, h2, h3};
+        int q = 0;
+        while (above + hs[q] < need) above += hs[q++];
+        s_digit = 255u - 4u * (unsigned)tid - (unsigned)q;
+        s_above = above;
+      }
+    }
+    __syncthreads();
+    prefix |= (unsigned long long)s_digit << shift;
+    pmask |= 255ull << shift;
+    need -= s_above;
+    __syncthreads();
+  }
+  // prefix = the K-th largest key: exactly K keys are >= it (keys are unique)
+  if (tid == 0) s_n = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (k[j] != 0 && k[j] >= prefix) sel[atomicAdd(&s_n, 1u)] = k[j];
+  __syncthreads();
+  int n2 = 1;
+  while (n2 < K) n2 <<= 1;
+  for (int i = K + tid; i < n2; i += kTopkThreads) sel[i] = 0;
+  __syncthreads();
+  // bitonic sort, descending
+  for (int size = 2; size <= n2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < n2; i += kTopkThreads) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const unsigned long long x = sel[i], y = sel[j];
+          if (desc ? x < y : x > y) {
+            sel[i] = y;
+            sel[j] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int r = tid; r < K; r += kTopkThreads) {
+    const unsigned long long key = sel[r];
+    skeys[seg + r] = (uint32_t)(key >> 32);
+    sidx[seg + r] = (int)(seg + (0xFFFFFFFFu - (uint32_t)key));
+  }
 }
 
 __global__ void segment_offsets(int* off, int B, int A) {
@@ -379,9 +470,20 @@ int launch_yolact_fast_nms(const float* cls, long long cls_bstride, int A, int C
   TV_HIP(hipGetLastError());
   hipLaunchKernelGGL(yolact::segment_offsets, dim3((B + 256) / 256), dim3(256), 0, s, offs, B, A);
   TV_HIP(hipGetLastError());
-  size_t tb = L.tmp_bytes;
-  TV_HIP(rocprim::segmented_radix_sort_pairs_desc(w + L.tmp, tb, keys, skeys, rocprim::counting_iterator<int>(0),
-                                                  sidx, n, (unsigned)B, offs, offs + 1, 0, 32, s));
+  if (K <= yolact::kTopkMaxK && A <= 32 * yolact::kTopkThreads) {
+    // (first K entries of each segment: all nms_iou / nms_compact read)
+    if (A <= 8 * yolact::kTopkThreads)
+      hipLaunchKernelGGL(yolact::nms_topk<8>, dim3(B), dim3(yolact::kTopkThreads), 0, s, keys, A, K, skeys, sidx);
+    else if (A <= 16 * yolact::kTopkThreads)
+      hipLaunchKernelGGL(yolact::nms_topk<16>, dim3(B), dim3(yolact::kTopkThreads), 0, s, keys, A, K, skeys, sidx);
+    else
+      hipLaunchKernelGGL(yolact::nms_topk<32>, dim3(B), dim3(yolact::kTopkThreads), 0, s, keys, A, K, skeys, sidx);
+    TV_HIP(hipGetLastError());
+  } else {
+    size_t tb = L.tmp_bytes;
+    TV_HIP(rocprim::segmented_radix_sort_pairs_desc(w + L.tmp, tb, keys, skeys, rocprim::counting_iterator<int>(0),
+                                                    sidx, n, (unsigned)B, offs, offs + 1, 0, 32, s));
+  }
   hipLaunchKernelGGL(yolact::nms_iou, dim3((K + yolact::kIouThreads - 1) / yolact::kIouThreads, B),
                      dim3(yolact::kIouThreads), 0, s, box, box_bstride, A, K, skeys, sidx, iou_thr, conf_thr, keep);
   TV_HIP(hipGetLastError());

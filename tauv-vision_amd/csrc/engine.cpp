@@ -1064,8 +1064,17 @@ const char* Engine::op_kernel(int B, size_t i) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->dcn_skip[i]) name = "(sampled inside the fused DCNv2 kernel)";
-      else if (ws->dcn[i].x) name = std::string(dcn64_mode && ws->dcn[i].C % 64 == 0 ? "tv::dcn::dcn_gemm64<" : "tv::dcn::dcn_gemm<") + t +
-               (ws->dcn[i].N % 128 == 0 ? ", 128>" : ", 64>");
+      else if (ws->dcn[i].x) {
+        const DcnParams& d = ws->dcn[i];
+        const bool wide = d.N % 128 == 0;
+        if (dcn64_mode && d.C % 64 == 0) {  // dcn_gemm64<T, BN, PX>: the pixel tile as launch_dcn_gemm picks it
+          const long tiles128 = ((long)d.B * d.H * d.W + 127) / 128 * (d.N / 128);
+          const int px = !wide || dcn64_mode == 2 || tiles128 < 1024 ? 64 : 128;
+          name = std::string("tv::dcn::dcn_gemm64<") + t + (wide ? ", 128, " : ", 64, ") + std::to_string(px) + ">";
+        } else {
+          name = std::string("tv::dcn::dcn_gemm<") + t + (wide ? ", 128>" : ", 64>");
+        }
+      }
       else if (ws->small[i])
         name = std::string("tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";

@@ -6,7 +6,7 @@ mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 for rep in 1 2; do
   for L in "$@"; do
-    TV_LIB=$GRAFT_REPO_ROOT/tauv-vision_amd/$L/libtauv_vision_amd.so timeout -k 10 120 python tools/kern_ab.py --tag "$L.$rep" --ops $O/ops_$L.$rep.json >> $O/ab.jsonl 2> $O/err_$L.log
+    TV_LIB=$GRAFT_REPO_ROOT/tauv-vision_amd/$L/libtauv_vision_amd.so timeout -k 10 120 python tools/kern_ab.py --model ${MODEL:-r18} --tag "$L.$rep" --ops $O/ops_$L.$rep.json >> $O/ab.jsonl 2> $O/err_$L.log
     rc=$?
     echo "$L.$rep rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 $O/err_$L.log; exit $rc; fi

@@ -9,5 +9,5 @@ rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|FAILED" $O/tests.log | tail -
 if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
 timeout -k 10 300 bash tools/gpu_libab.sh $TAG/ab lib $ALT > $O/ab.log 2>&1; rc=$?; echo "ab rc=$rc"; tail -16 $O/ab.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-BENCH_PROFILE_OUT=$O/ops_r18.json timeout -k 10 400 python bench.py --no-cpu-baseline --no-b1 > $O/bench.log 2>&1; echo "bench rc=$?"
+BENCH_PROFILE_OUT=$O/ops_r18.json timeout -k 10 400 python bench.py --model ${MODEL:-r18} --no-cpu-baseline --no-b1 > $O/bench.log 2>&1; echo "bench rc=$?"
 tail -1 $O/bench.log | cut -c1-700

@@ -111,12 +111,18 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
   int cur_seg = -1;
   lds_char* const ring = lds + grp * GRP_RING;
 
-  // k-step kbeg + j of this group into ring slot `slot`
-  auto issue = [&](int j, int slot) __attribute__((always_inline)) {
-    const int ks = kbeg + j;
+  // k-step descriptors (scalar loads) are fetched one k-step before their DMA is issued: a cold
+  // descriptor is an L2 / MALL round trip, which on the issue path delayed every k-step's DMA
+  // (the latency chain these tiny layers are bound by). Past the layer's end: its last step.
+  auto load_desc = [&](int j) __attribute__((always_inline)) -> KStep {
+    const int ks = min(kbeg + j, p.nks - 1);
     c_u32x4* kq = (c_u32x4*)(kdesc + ks);
     struct { u32x4 q[5]; } raw = {{kq[0], kq[1], kq[2], kq[3], kq[4]}};
-    const KStep d = __builtin_bit_cast(KStep, raw);
+    return __builtin_bit_cast(KStep, raw);
+  };
+  // k-step kbeg + j (descriptor d) of this group into ring slot `slot`
+  auto issue = [&](int j, int slot, const KStep& d) __attribute__((always_inline)) {
+    const int ks = kbeg + j;
     if (d.seg != cur_seg) {
       cur_seg = d.seg;
       const T* src = reinterpret_cast<const T*>(d.src);
@@ -178,13 +184,15 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
   };
   // iteration j (both groups run `half` iterations so every wave meets every barrier; group 1
   // idles through its last one when nks is odd): stage j's fragments are in `cur`
+  KStep dn;  // descriptor of the next k-step to issue
   auto step = [&](int j, u32x4(&cur)[4][3], u32x4(&nxt)[4][3]) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (j + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");  // stage j+1 landed
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage j+1 visible to the group, slot j%S released
     __builtin_amdgcn_sched_barrier(0);
-    if (j + S < nk) issue(j + S, j % S);
+    if (j + S < nk) issue(j + S, j % S, dn);
+    if (j + S + 1 < nk) dn = load_desc(j + S + 1);  // waited at the next step's lgkmcnt(0)
     if (j + 1 < nk) read_frags(j + 1, nxt);
     __builtin_amdgcn_sched_barrier(0);
     if (j < nk) mfmas(cur);
@@ -192,7 +200,12 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
   };
 
   const int npro = nk < S ? nk : S;
-  for (int s = 0; s < npro; ++s) issue(s, s);
+  static_assert(S == 3, "prologue descriptors");
+  const KStep d0 = load_desc(0), d1 = load_desc(1), d2 = load_desc(2);  // all in flight at once
+  dn = load_desc(S);
+  if (npro > 0) issue(0, 0, d0);
+  if (npro > 1) issue(1, 1, d1);
+  if (npro > 2) issue(2, 2, d2);
   if (npro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
   else if (npro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -90,6 +90,12 @@ struct ConvParams {
   int head_ldc;
   int head_row0[16], head_nrows[16];
   unsigned long long* dbg;  // diagnostic stamp builds only (conv3x3 TV_C3_EXP == 9): per-wave cycle buckets
+  // conv_lat split-K over workgroups: ksplit workgroups per tile each walk a slice of the k-steps,
+  // write their fp32 partial tile to slab[tile][slice] (write-through), and the last to arrive
+  // (cnt[tile], agent-scope counter, zero before the launch) sums the slices in slice order
+  int ksplit;
+  float* slab;
+  unsigned* cnt;
 };
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
@@ -101,6 +107,8 @@ constexpr int kPipeTileM = 256;
 // mode-0 k-steps only (every segment's channel count a multiple of 64 / 128 bytes)
 int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles);
 int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s);
+// fp32 slab floats one conv_lat split-K tile slice needs (64 x 128)
+constexpr int kLatSlabFloats = 64 * 128;
 
 // Persistent halo-tile 3x3 / stride 1 / pad 1 kernel (conv3x3.hip), fp16/bf16, 128- or 256-channel
 // input (seg[0].C): 512-pixel

@@ -32,7 +32,7 @@ constexpr int GA = PX / 8 / 4;               // A pieces (1 KiB) per wave per k-
 constexpr int GB = CH / 8 / 4;               // B pieces per wave per k-step = 4
 constexpr int G = GA + GB;                   // LDS-DMA instructions per wave per k-step
 constexpr int SR = CH + 4;                   // staged fp32 row (floats)
-static_assert(PX * SR * 4 <= LDS, "reduction tile fits the ring");
+static_assert(PX * SR * 4 <= LDS - 16, "reduction tile fits the ring (below the split-K ticket word)");
 
 typedef __attribute__((address_space(3))) char lds_char;
 typedef const __attribute__((address_space(1))) void gvoid;
@@ -47,6 +47,10 @@ __device__ __forceinline__ u32x4 ds_read16(unsigned addr) {
   return v;
 }
 __device__ __forceinline__ uint4 to_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;  // global (never flat) agent-scope ticket words
+__device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 
 template <typename T>
 __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__ pp) {
@@ -65,19 +69,24 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
 
   // XCD-aware order: contiguous runs of the linear tile index per XCD, the channel tiles of a
   // pixel tile adjacent (they read the same input pixels)
-  const int nbk = p.mtiles * p.ntiles;
+  // (split-K: the ksplit slices of a tile adjacent too, so they tend to share an XCD — speed only)
+  const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
+  const int nbk = p.mtiles * p.ntiles * ksplit;
   const int bid = blockIdx.x;
   const int q8 = nbk >> 3, r8 = nbk & 7, xcd = bid & 7;
-  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int lin_s = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int lin = lin_s / ksplit;      // tile
+  const int slice = lin_s - lin * ksplit;
   const int ntile = lin % p.ntiles;
   const int mtile = lin / p.ntiles;
   const int m0 = mtile * PX;
   const int n0 = ntile * CH;
 
-  // K range of this group
-  const int half = (p.nks + 1) >> 1;
-  const int kbeg = grp * half;
-  const int nk = grp ? p.nks - half : half;  // wave-uniform; group 1 may have one step fewer
+  // K range of this slice, then of this group
+  const int ks0 = (int)((long)p.nks * slice / ksplit), ks1 = (int)((long)p.nks * (slice + 1) / ksplit);
+  const int half = (ks1 - ks0 + 1) >> 1;
+  const int kbeg = ks0 + grp * half;
+  const int nk = grp ? (ks1 - ks0) - half : half;  // wave-uniform; group 1 may have one step fewer
 
   // ---- DMA geometry: A piece i of this wave covers tile rows (wq*GA + i)*8 + lane/8; the lane's
   // LDS chunk is lane%8 and it fetches source chunk (lane%8) ^ ((row>>1)&7) of that row
@@ -202,10 +211,10 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
   const int npro = nk < S ? nk : S;
   static_assert(S == 3, "prologue descriptors");
   const KStep d0 = load_desc(0), d1 = load_desc(1), d2 = load_desc(2);  // all in flight at once
-  dn = load_desc(S);
   if (npro > 0) issue(0, 0, d0);
   if (npro > 1) issue(1, 1, d1);
   if (npro > 2) issue(2, 2, d2);
+  dn = load_desc(S);
   if (npro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
   else if (npro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -243,18 +252,90 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
       }
   }
   __syncthreads();
+  constexpr int RPT = PX * (CH / 8) / NT;  // 8-channel chunks per thread (2)
+  f32x4 xs[RPT][2];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int it = tid + r * NT;
+    const float* sv = stg + (it >> 4) * SR + (it & 15) * 8;
+    xs[r][0] = *reinterpret_cast<const f32x4*>(sv);
+    xs[r][1] = *reinterpret_cast<const f32x4*>(sv + 4);
+  }
+  if (ksplit > 1) {
+    // Split-K hand-off (cdna_hip_programming.md §6 Guideline 16, write-through form): this slice's
+    // partial tile goes to slab[tile][slice] with sc1 stores (no release fence), every storing
+    // wave drains them (vmcnt(0)), the workgroup barrier orders that before ONE relaxed agent-scope
+    // ticket; the workgroup drawing ksplit - 1 sums every slice in slice order 0, 1, ... (its own
+    // from registers, the others by sc1 loads: bit-identical whichever workgroup arrives last) and
+    // resets the ticket. The engine also zeroes the tickets before each forward.
+    i32x4 rs;
+    {
+      const unsigned long long a = (unsigned long long)(p.slab + (size_t)lin * ksplit * (PX * CH));
+      rs.x = (int)(unsigned)a;
+      rs.y = (int)(unsigned)(a >> 32);
+      rs.z = ksplit * PX * CH * 4;
+      rs.w = 0x00020000;
+    }
+    constexpr int SC1 = 16;  // aux cache bits: sc1 (write-through store / L1-bypassing load)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int it = tid + r * NT;
+      if (m0 + (it >> 4) >= p.M) continue;  // only live rows travel
+      const int off = (slice * (PX * CH) + it * 8) * 4;
+      raw_buffer_store_v4(__builtin_bit_cast(u32x4, xs[r][0]), rs, off, 0, SC1);
+      raw_buffer_store_v4(__builtin_bit_cast(u32x4, xs[r][1]), rs, off + 16, 0, SC1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its slab bytes landed
+    __syncthreads();
+    unsigned* last_flag = reinterpret_cast<unsigned*>(smem + LDS - 16);
+    if (tid == 0) {
+      const unsigned t = __hip_atomic_fetch_add((gu32*)(p.cnt + lin), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last_flag = t;
+    }
+    __syncthreads();
+    if (*last_flag != (unsigned)(ksplit - 1)) return;  // workgroup-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: every slab load below is sc1
+    f32x4 sum[RPT][2];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) sum[r][0] = sum[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < ksplit; ++q) {
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const int it = tid + r * NT;
+        f32x4 a0 = xs[r][0], a1 = xs[r][1];
+        if (q != slice) {
+          const int off = (q * (PX * CH) + it * 8) * 4;
+          const bool live = m0 + (it >> 4) < p.M;
+          a0 = __builtin_bit_cast(f32x4, raw_buffer_load_v4(rs, live ? off : (int)0x80000000u, 0, SC1));
+          a1 = __builtin_bit_cast(f32x4, raw_buffer_load_v4(rs, live ? off + 16 : (int)0x80000000u, 0, SC1));
+        }
+        if (q == 0) {
+          sum[r][0] = a0;
+          sum[r][1] = a1;
+        } else {
+          sum[r][0] += a0;
+          sum[r][1] += a1;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      xs[r][0] = sum[r][0];
+      xs[r][1] = sum[r][1];
+    }
+    if (tid == 0) __hip_atomic_store((gu32*)(p.cnt + lin), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   // bias + activation + 16-byte stores: 64 pixels x 16 chunks of 8 channels, 2 per thread
   T* const out = reinterpret_cast<T*>(p.out);
 #pragma unroll
-  for (int r = 0; r < PX * (CH / 8) / NT; ++r) {
+  for (int r = 0; r < RPT; ++r) {
     const int it = tid + r * NT;
     const int px = it >> 4, c8 = (it & 15) * 8;
     const int m = m0 + px;
     const int n = n0 + c8;
     if (m >= p.M || n >= p.N) continue;
-    const float* sv = stg + px * SR + c8;
-    const f32x4 x0 = *reinterpret_cast<const f32x4*>(sv);
-    const f32x4 x1 = *reinterpret_cast<const f32x4*>(sv + 4);
+    const f32x4 x0 = xs[r][0];
+    const f32x4 x1 = xs[r][1];
     const uint4 b0 = gload16(p.bias + n), b1 = gload16(p.bias + n + 4);
     float v[8] = {x0[0] + __uint_as_float(b0.x), x0[1] + __uint_as_float(b0.y), x0[2] + __uint_as_float(b0.z),
                   x0[3] + __uint_as_float(b0.w), x1[0] + __uint_as_float(b1.x), x1[1] + __uint_as_float(b1.y),
@@ -271,7 +352,7 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
 template <typename T>
 static int launch_t(const ConvParams& p, const ConvParams* dp, hipStream_t s) {
   if (int r = ensure_lds<conv_lat<T>>(LDS)) return r;
-  hipLaunchKernelGGL(conv_lat<T>, dim3(p.mtiles * p.ntiles), dim3(NT), LDS, s, dp);
+  hipLaunchKernelGGL(conv_lat<T>, dim3(p.mtiles * p.ntiles * (p.ksplit > 1 ? p.ksplit : 1)), dim3(NT), LDS, s, dp);
   TV_HIP(hipGetLastError());
   return 0;
 }
@@ -286,7 +367,7 @@ int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles) {
 
 int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s) {
   if (!p.ks || p.nks <= 0 || p.mtiles != (p.M + lat::PX - 1) / lat::PX || p.ntiles * lat::CH < p.N || p.N % 8 ||
-      p.out_ldc % 8 || p.out_coff % 8 || !p.out) {
+      p.out_ldc % 8 || p.out_coff % 8 || !p.out || (p.ksplit > 1 && (!p.slab || !p.cnt || p.ksplit > p.nks))) {
     set_error("conv_lat: inconsistent launch geometry");
     return 1;
   }

@@ -114,11 +114,16 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
 #pragma unroll
   for (int i = 0; i < GB; ++i) woff[i] = (uint32_t)(wsrc[i] - wbase);
 
-  auto issue = [&](int ks, int slot) __attribute__((always_inline)) {
-    // wave-uniform descriptor: 80 bytes by scalar loads (constant address space)
-    const __attribute__((address_space(4))) u32x4* kq = (const __attribute__((address_space(4))) u32x4*)(kdesc + ks);
+  // wave-uniform descriptor: 80 bytes by scalar loads (constant address space), fetched one
+  // k-step before its DMA is issued (the prologue's three at once): a cold descriptor is an L2 /
+  // MALL round trip that otherwise sits on every k-step's issue path. Past the end: the last one.
+  auto load_desc = [&](int ks) __attribute__((always_inline)) -> KStep {
+    const __attribute__((address_space(4))) u32x4* kq =
+        (const __attribute__((address_space(4))) u32x4*)(kdesc + min(ks, total_ks - 1));
     struct { u32x4 q[5]; } raw = {{kq[0], kq[1], kq[2], kq[3], kq[4]}};
-    const KStep d = __builtin_bit_cast(KStep, raw);
+    return __builtin_bit_cast(KStep, raw);
+  };
+  auto issue = [&](int ks, int slot, const KStep& d) __attribute__((always_inline)) {
     const T* src = reinterpret_cast<const T*>(d.src);
     lds_char* abase = lds + slot * STAGE + wave * GA * 1024;
     if (d.mode == 0) {
@@ -210,6 +215,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
 #pragma unroll
         for (int b = 0; b < 2; ++b) Mfma<T>::run(to_u4(f[j][a]), to_u4(f[j][2 + b]), acc[a][b]);
   };
+  KStep dn;  // descriptor of the next k-step to issue
   // one k-step: stage ks's fragments are in `cur`; DMA keeps stages ks+2, ks+3 in flight
   auto step = [&](int ks, u32x4(&cur)[4][4], u32x4(&nxt)[4][4]) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage ks landed
@@ -217,7 +223,8 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // every wave: stage ks+1 visible, slot ks%S released
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + S < total_ks) issue(ks + S, ks % S);
+    if (ks + S < total_ks) issue(ks + S, ks % S, dn);
+    if (ks + S + 1 < total_ks) dn = load_desc(ks + S + 1);  // waited at the next step's lgkmcnt(0)
     if (ks + 1 < total_ks) read_frags(ks + 1, nxt);
     __builtin_amdgcn_sched_barrier(0);
     mfmas(cur);
@@ -225,7 +232,12 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   };
 
   const int npro = total_ks < S ? total_ks : S;
-  for (int s = 0; s < npro; ++s) issue(s, s);
+  static_assert(S == 3, "prologue descriptors");
+  const KStep d0 = load_desc(0), d1 = load_desc(1), d2 = load_desc(2);  // all in flight at once
+  if (npro > 0) issue(0, 0, d0);
+  if (npro > 1) issue(1, 1, d1);
+  if (npro > 2) issue(2, 2, d2);
+  dn = load_desc(S);
   if (npro >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
   else if (npro == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

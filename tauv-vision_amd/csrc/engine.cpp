@@ -305,6 +305,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_STEM") stem_mode = v;
     else if (k == "TV_LAT") lat_mode = v;
     else if (k == "TV_LAT_UNITS") lat_units = v;
+    else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
     else if (k == "TV_DCN64") dcn64_mode = v;
     else if (k == "TV_CONVT") convt_mode = v;
     else if (k == "TV_CONV3S2") s2_mode = v;
@@ -364,6 +365,8 @@ Engine::~Engine() {
     if (kv.second->arena) (void)hipFree(kv.second->arena);
     if (kv.second->dparams) (void)hipFree(kv.second->dparams);
     if (kv.second->dks) (void)hipFree(kv.second->dks);
+    if (kv.second->slab) (void)hipFree(kv.second->slab);
+    if (kv.second->cnt) (void)hipFree(kv.second->cnt);
     delete kv.second;
   }
   for (auto& kv : side) {
@@ -808,6 +811,35 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->s2_grid[i] = 0;
     ws->lat[i] = 1;
   }
+  // conv_lat split-K over workgroups for the layers whose tiles leave most CUs idle (the latency
+  // path: at B=1 every conv_lat layer is one k-step chain of ~9 latency-bound k-steps per K group):
+  // up to lat_split_max workgroups per tile, each slice >= 2 k-steps (one per K group), the tiles x
+  // slices within one round of CUs. Partial tiles meet in `slab`, tickets in `cnt` (conv_lat.hip).
+  {
+    size_t slab_floats = 0, tickets = 0;
+    for (size_t i = 0; i < plan.ops.size(); ++i) {
+      if (!ws->lat[i]) continue;
+      ConvParams& p = ws->params[i];
+      const int tiles = p.mtiles * p.ntiles;
+      int ks = std::min(lat_split_max, p.nks / 2);
+      ks = std::min(ks, cu_count / std::max(1, tiles));
+      p.ksplit = ks > 1 ? ks : 0;
+      if (!p.ksplit) continue;
+      slab_floats = std::max(slab_floats, (size_t)tiles * ks * kLatSlabFloats);
+      tickets = std::max(tickets, (size_t)tiles);
+    }
+    if (tickets) {
+      ws->cnt_bytes = align_up(tickets * sizeof(unsigned), 16);
+      TV_HIP(hipMalloc((void**)&ws->slab, slab_floats * sizeof(float)));
+      TV_HIP(hipMalloc((void**)&ws->cnt, ws->cnt_bytes));
+      TV_HIP(hipMemset(ws->cnt, 0, ws->cnt_bytes));
+      for (size_t i = 0; i < plan.ops.size(); ++i)
+        if (ws->lat[i] && ws->params[i].ksplit) {
+          ws->params[i].slab = ws->slab;
+          ws->params[i].cnt = ws->cnt;
+        }
+    }
+  }
   if (stamp_op >= 0 && stamp_op < (int)plan.ops.size() && ws->c3_tw[stamp_op]) ws->params[stamp_op].dbg = stamp_buf;
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
@@ -834,6 +866,8 @@ int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
     if (ws->arena) (void)hipFree(ws->arena);
     if (ws->dparams) (void)hipFree(ws->dparams);
     if (ws->dks) (void)hipFree(ws->dks);
+    if (ws->slab) (void)hipFree(ws->slab);
+    if (ws->cnt) (void)hipFree(ws->cnt);
     delete ws;
     return rc;
   }
@@ -850,6 +884,8 @@ int Engine::trim() {
     if (kv.second->arena) (void)hipFree(kv.second->arena);
     if (kv.second->dparams) (void)hipFree(kv.second->dparams);
     if (kv.second->dks) (void)hipFree(kv.second->dks);
+    if (kv.second->slab) (void)hipFree(kv.second->slab);
+    if (kv.second->cnt) (void)hipFree(kv.second->cnt);
     delete kv.second;
   }
   workspaces.clear();
@@ -973,6 +1009,9 @@ int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStrea
   Workspace* ws = nullptr;
   int rc = get_workspace(B, s, &ws);
   if (rc) return rc;
+  // conv_lat split-K tickets start every forward at zero (a memset node under capture; each
+  // tile's last slice also resets its own)
+  if (ws->cnt && op0 == 0) TV_HIP(hipMemsetAsync(ws->cnt, 0, ws->cnt_bytes, s));
   for (size_t i = op0; i < plan.ops.size() && i < op1; ++i) {
     rc = run_op(i, ws, input, input_u8, out, s);
     if (rc) return rc;

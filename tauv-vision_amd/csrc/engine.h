@@ -49,6 +49,9 @@ struct Workspace {
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
   std::vector<ConvTParams> tparams; // per op: convt.hip launch parameters
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
+  float* slab = nullptr;            // conv_lat split-K partial tiles (ops run in order: one buffer)
+  unsigned* cnt = nullptr;          // conv_lat split-K tickets, one per tile, zeroed per forward
+  size_t cnt_bytes = 0;
   std::vector<std::string> kname;   // per op: kernel instance name (diagnostics), filled lazily
 };
 
@@ -78,6 +81,7 @@ struct Engine {
                                // (env TV_LAT=0 off)
   int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (env TV_DCN64=0 off)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
+  int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)
   int stamp_op = -1;           // diagnostics: op whose conv3x3 launch gets a stamp buffer (knob TV_C3_STAMPS=op:ptr)
   unsigned long long* stamp_buf = nullptr;
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)

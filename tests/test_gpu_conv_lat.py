@@ -69,3 +69,28 @@ def test_lat_default_selection_b32():
     assert kern["backbone.dla_down.tree_layers.4.tree_r.root.conv"].startswith("tv::lat::conv_lat<"), kern
     assert kern["backbone.dla_down.tree_layers.0.tree_l.tree_r.conv1"].startswith("tv::c3::conv3x3<"), kern
     assert kern["backbone.multi_ida_up.ida_up_layers.0.output_layers.0.0"].startswith("tv::c3::conv3x3<"), kern
+
+
+def test_lat_split_k_b1(monkeypatch):
+    """At B=1 the conv_lat layers run split-K over workgroups (several workgroups per tile, the
+    last to arrive sums the fp32 partial tiles in slice order): repeated forwards are bit-identical
+    whichever workgroup arrives last, and the result matches the unsplit kernel (knob
+    TV_LAT_SPLIT=1) within the fp16 tolerance of the golden comparison."""
+    from tauv_vision_amd import engine as E
+    name = "r18_c128_b1_480x640"
+    img = case_input(name).cuda()
+    model, oc, mc, case = fwd.build(name, "fp16")
+    runs = [model(img) for _ in range(3)]
+    for f in ("heatmap", "size", "offset"):
+        for r in runs[1:]:
+            assert torch.equal(getattr(r, f), getattr(runs[0], f)), f
+    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_LAT_SPLIT": "1"})
+    model1, _, _, _ = fwd.build(name, "fp16")
+    ref = model1(img)
+    g = golden(f"model_{name}")
+    for f in ("heatmap", "size", "offset"):
+        scale = max(1.0, float(abs(g[f]).max()))
+        d = float((getattr(runs[0], f) - getattr(ref, f)).abs().max())
+        assert d <= fwd.TOL["fp16"] * scale, (f, d)
+        got = getattr(runs[0], f).detach().cpu().numpy()
+        assert float(abs(got - g[f]).max()) <= fwd.TOL["fp16"] * scale, f

@@ -208,6 +208,17 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // this thread's epilogue bias chunks, loaded up front: issued after the loop they were one more
+  // memory round trip at the end of a latency-bound kernel
+  constexpr int RPT = PX * (CH / 8) / NT;  // 8-channel output chunks per thread (2)
+  uint4 bpre[RPT][2];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int n = n0 + ((tid + r * NT) & 15) * 8;
+    const bool ok = n < p.N;
+    bpre[r][0] = ok ? gload16(p.bias + n) : make_uint4(0, 0, 0, 0);
+    bpre[r][1] = ok ? gload16(p.bias + n + 4) : make_uint4(0, 0, 0, 0);
+  }
   const int npro = nk < S ? nk : S;
   static_assert(S == 3, "prologue descriptors");
   const KStep d0 = load_desc(0), d1 = load_desc(1), d2 = load_desc(2);  // all in flight at once
@@ -252,7 +263,6 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
       }
   }
   __syncthreads();
-  constexpr int RPT = PX * (CH / 8) / NT;  // 8-channel chunks per thread (2)
   f32x4 xs[RPT][2];
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
@@ -336,7 +346,7 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
     if (m >= p.M || n >= p.N) continue;
     const f32x4 x0 = xs[r][0];
     const f32x4 x1 = xs[r][1];
-    const uint4 b0 = gload16(p.bias + n), b1 = gload16(p.bias + n + 4);
+    const uint4 b0 = bpre[r][0], b1 = bpre[r][1];
     float v[8] = {x0[0] + __uint_as_float(b0.x), x0[1] + __uint_as_float(b0.y), x0[2] + __uint_as_float(b0.z),
                   x0[3] + __uint_as_float(b0.w), x1[0] + __uint_as_float(b1.x), x1[1] + __uint_as_float(b1.y),
                   x1[2] + __uint_as_float(b1.z), x1[3] + __uint_as_float(b1.w)};

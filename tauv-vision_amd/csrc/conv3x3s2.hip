@@ -66,6 +66,39 @@ constexpr int BLK_PB[NBLK] = {0, 0, 3, 1, 1, 3, 2, 2};  // phase block: 0 (1,1),
 constexpr int BLK_CB[NBLK] = {0, 1, 0, 0, 1, 1, 0, 1};  // channel block within the pair
 constexpr int PB_LEN[4] = {4, 2, 2, 1};
 constexpr int PB_J0[4] = {0, 4, 6, 8};                // first k-step j of the phase block
+#ifndef TV_S2_SPREAD
+#define TV_S2_SPREAD 0  // 0: all at the first step; 1: a block's 6 halo pieces spread over its first two k-steps where the cover allows
+#endif
+// Halo pieces of block b + 2 issued at step t of block b (position b8 in the pair), HPW in all.
+// Default: all at the block's first step. TV_S2_SPREAD: 3 + 3 over the first two steps of a
+// 4-step block, and of a 2-step block followed by one of >= 2 steps (the second half still has
+// >= 2 steps of cover before block b + 2 starts); the 1-step blocks and a 2-step block before a
+// 1-step one keep all 6 at their first step.
+constexpr int piece_cnt(int b8, int t) {
+  const int L = PB_LEN[BLK_PB[b8]], Ln = PB_LEN[BLK_PB[(b8 + 1) % NBLK]];
+  if (TV_S2_SPREAD && (L >= 4 || (L == 2 && Ln >= 2))) return t == 0 ? 3 : t == 1 ? HPW - 3 : 0;
+  return t == 0 ? HPW : 0;
+}
+constexpr int piece_p0(int b8, int t) {
+  int p = 0;
+  for (int u = 0; u < t; ++u) p += piece_cnt(b8, u);
+  return p;
+}
+constexpr int piece_tlast(int b8) {
+  int tl = 0;
+  for (int u = 0; u < PB_LEN[BLK_PB[b8]]; ++u)
+    if (piece_cnt(b8, u) > 0) tl = u;
+  return tl;
+}
+// VMEM operations issued after the last piece of block B + 1's halo when block B's last k-step
+// starts (exact; block B + 1 was issued during block B - 1): that step's weight load, the weight
+// loads of block B - 1's later steps, then every earlier step of block B: its pieces and its load
+constexpr int younger_of(int b8) {
+  const int bp = (b8 + NBLK - 1) % NBLK;
+  int y = 1 + (PB_LEN[BLK_PB[bp]] - 1 - piece_tlast(bp));
+  for (int t = 0; t + 1 < PB_LEN[BLK_PB[b8]]; ++t) y += piece_cnt(b8, t) + 1;
+  return y;
+}
 struct Sched {
   int cb[SPT], j[SPT], blk[SPT], t[SPT];
 };
@@ -366,7 +399,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     // issued at the start of the previous block, before that step's weight load; since then one
     // weight load per k-step and, if this block is longer than one k-step, this block's own issue
     // (at its first step, before that step's weight load)
-    constexpr int YOUNGER = LPREV + L - 1 + (L >= 2 ? HPW : 0);
+    constexpr int YOUNGER = younger_of(B8);
+    static_assert(TV_S2_SPREAD || YOUNGER == LPREV + L - 1 + (L >= 2 ? HPW : 0), "the all-at-first-step count");
     static_assert(YOUNGER <= 13, "wait_vm_n range");
     if constexpr (BOUNDARY) wait_vm_n(s + 1 < S_tot ? YOUNGER : 0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -388,11 +422,15 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     constexpr int NB = BLK + 2, NB8 = NB % NBLK;
     constexpr bool NEXT_TILE = NB >= 2 * NBLK;
     constexpr int ICB = 2 * ((NB % (2 * NBLK)) / NBLK) + BLK_CB[NB8], IPB = BLK_PB[NB8];
+    // this step's pieces [P0, P1) of block BLK + 2, split over the three issue points
+    constexpr int P0 = piece_p0(B8, TB), P1 = P0 + piece_cnt(B8, TB);
     auto issue_part = [&](auto lo, auto hi) __attribute__((always_inline)) {
-      if constexpr (TB == 0) {
+      constexpr int LO = decltype(lo)::value > P0 ? decltype(lo)::value : P0;
+      constexpr int HI = decltype(hi)::value < P1 ? decltype(hi)::value : P1;
+      if constexpr (LO < HI) {
         const int tbuf = buf == 0 ? 2 : buf - 1;  // (buf + 2) % 3
-        if constexpr (NEXT_TILE) issue_block(nx_fr, nx_y0, nx_x0, ICB, IPB, tbuf, lo, hi);  // (last tile: itself, into a free buffer)
-        else issue_block(cur_fr, cur_y0, cur_x0, ICB, IPB, tbuf, lo, hi);
+        if constexpr (NEXT_TILE) issue_block(nx_fr, nx_y0, nx_x0, ICB, IPB, tbuf, IC<LO>{}, IC<HI>{});  // (last tile: itself, into a free buffer)
+        else issue_block(cur_fr, cur_y0, cur_x0, ICB, IPB, tbuf, IC<LO>{}, IC<HI>{});
       }
     };
     mfma_pair(IC<0>{}, IC<FIRST>{}, H0);

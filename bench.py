@@ -608,6 +608,12 @@ def env_knobs():
     return {k: v for k, v in sorted(os.environ.items()) if k.startswith("TV_")}
 
 
+# TV_* variables that select a library build rather than an engine knob: TV_LIB (this script and
+# tools/), TV_TEST_LIB (tests/conftest.py). Everything else is forwarded to the engine, which
+# refuses names it does not know.
+PACKAGE_KNOBS = ("TV_LIB", "TV_TEST_LIB")
+
+
 def forward_env_knobs(knobs):
     """Diagnostics (A/B runs, tools/): hand TV_* knobs to the package explicitly — the library
     and the package read no environment. TV_LIB = another build of the library."""
@@ -617,7 +623,7 @@ def forward_env_knobs(knobs):
     from tauv_vision_amd.engine import set_diagnostic_knobs
     if "TV_LIB" in knobs:
         _lib.set_library_path(knobs["TV_LIB"])
-    set_diagnostic_knobs({k: v for k, v in knobs.items() if k != "TV_LIB"})
+    set_diagnostic_knobs({k: v for k, v in knobs.items() if k not in PACKAGE_KNOBS})
 
 
 def main():

@@ -67,7 +67,7 @@ constexpr int BLK_CB[NBLK] = {0, 1, 0, 0, 1, 1, 0, 1};  // channel block within 
 constexpr int PB_LEN[4] = {4, 2, 2, 1};
 constexpr int PB_J0[4] = {0, 4, 6, 8};                // first k-step j of the phase block
 #ifndef TV_S2_SPREAD
-#define TV_S2_SPREAD 0  // 0: all at the first step; 1: a block's 6 halo pieces spread over its first two k-steps where the cover allows
+#define TV_S2_SPREAD 1  // 0: all at the first step; 1 (default since round 4): a block's 6 halo pieces spread over its first two k-steps where the cover allows
 #endif
 // Halo pieces of block b + 2 issued at step t of block b (position b8 in the pair), HPW in all.
 // Default: all at the block's first step. TV_S2_SPREAD: 3 + 3 over the first two steps of a

@@ -317,9 +317,26 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_C3_HALF_COST") c3_half_cost = v;
     else if (k == "TV_SLICES") slices = std::max(1, std::min(kMaxSlices, v));
     else if (k == "TV_C3_STAMPS") {  // "op:device pointer" (stamp builds of conv3x3 only)
+#if defined(TV_C3_EXP) && TV_C3_EXP == 9
       stamp_op = v;
       const char* c = std::strchr(env, ':');
       stamp_buf = c ? reinterpret_cast<unsigned long long*>(std::strtoull(c + 1, nullptr, 0)) : nullptr;
+      // the stamp kernel writes 8 counters per wave of every workgroup it may launch (<= one per
+      // CU, 8 waves): the pointer must lie in a device allocation with that much room after it
+      hipDeviceptr_t base = nullptr;
+      size_t size = 0;
+      const size_t need = (size_t)cu_count * 8 * 8 * sizeof(unsigned long long);
+      if (!stamp_buf || hipMemGetAddressRange(&base, &size, stamp_buf) != hipSuccess ||
+          (char*)stamp_buf + need > (char*)base + size) {
+        (void)hipGetLastError();
+        set_error("TV_C3_STAMPS: the pointer is not inside a device allocation of >= " + std::to_string(need) +
+                  " bytes");
+        return TV_EINVAL;
+      }
+#else
+      set_error("TV_C3_STAMPS needs the stamp build of the library (EXTRA=-DTV_C3_EXP=9)");
+      return TV_EINVAL;
+#endif
     }
     else if (k == "TV_SLICE_SIZES") {
       for (const char* c = env; *c;) {

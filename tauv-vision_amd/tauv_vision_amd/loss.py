@@ -47,8 +47,23 @@ def _check_index(idx, valid, bound, what):
         raise IndexError(f"{what} out of range for {bound} planes")
 
 
+def _out_shape(model_config):
+    """The kernels derive the target grid as in_h // downsample_ratio x in_w // downsample_ratio
+    (the reference ModelConfig's out_h / out_w, config.py:24-30) and write it through raw pointers:
+    a duck-typed config whose out_h / out_w disagree would be written out of bounds."""
+    r = int(model_config.downsample_ratio)
+    if r < 1:
+        raise ValueError(f"downsample_ratio must be >= 1, got {r}")
+    H, W = int(model_config.in_h) // r, int(model_config.in_w) // r
+    if (int(model_config.out_h), int(model_config.out_w)) != (H, W):
+        raise ValueError(f"model_config.out_h/out_w = ({model_config.out_h}, {model_config.out_w}) but the "
+                         f"targets grid is in_h // downsample_ratio x in_w // downsample_ratio = ({H}, {W})")
+    return H, W
+
+
 def generate_heatmap(truth, model_config, train_config, object_config) -> torch.Tensor:
     """loss.py:31-72 -> [B, n_labels, out_h, out_w] fp32 on the GPU."""
+    H, W = _out_shape(model_config)
     dev = _device(truth.valid)
     B, n_obj = truth.valid.shape
     L = object_config.n_labels
@@ -57,7 +72,7 @@ def generate_heatmap(truth, model_config, train_config, object_config) -> torch.
     center = _as(truth.center, torch.float32, dev)
     _check_index(label, valid.bool(), L, "label")
     label = torch.where(label < 0, label + L, label)
-    out = torch.empty((B, L, model_config.out_h, model_config.out_w), dtype=torch.float32, device=dev)
+    out = torch.empty((B, L, H, W), dtype=torch.float32, device=dev)
     _lib.check(_lib.lib().tv_train_heatmap(
         ctypes.c_void_p(valid.data_ptr()), ctypes.c_void_p(label.data_ptr()), ctypes.c_void_p(center.data_ptr()),
         B, n_obj, L, model_config.in_h, model_config.in_w, model_config.downsample_ratio,
@@ -69,6 +84,7 @@ def generate_heatmap(truth, model_config, train_config, object_config) -> torch.
 def generate_keypoint_heatmap(truth, model_config, train_config, object_config):
     """loss.py:75-135 -> (heatmap, affinity_weight [B, n_keypoints, out_h, out_w],
     affinity [B, n_keypoints, 2, out_h, out_w]) fp32 on the GPU."""
+    H, W = _out_shape(model_config)
     dev = _device(truth.keypoint_valid)
     B, n_inst = truth.keypoint_valid.shape
     n_obj = truth.center.shape[1]
@@ -82,7 +98,6 @@ def generate_keypoint_heatmap(truth, model_config, train_config, object_config):
     _check_index(kobj, kvalid.bool(), n_obj, "keypoint_object_index")
     klabel = torch.where(klabel < 0, klabel + K, klabel)
     kobj = torch.where(kobj < 0, kobj + n_obj, kobj)
-    H, W = model_config.out_h, model_config.out_w
     heat = torch.empty((B, K, H, W), dtype=torch.float32, device=dev)
     aw = torch.empty_like(heat)
     aff = torch.empty((B, K, 2, H, W), dtype=torch.float32, device=dev)

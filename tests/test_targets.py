@@ -73,6 +73,45 @@ def test_gpu_targets_match_reference(name):
     np.testing.assert_array_equal(L.out_index_for_position(truth.center, mc).cpu().numpy(), g["out_index"])
 
 
+# One element behind the 2e-7 tolerance above (float32 bits 0x3fee9794 = 1.8640008): torch's CPU
+# sqrt (MKL VML on this image, AVX512) returns 1.3652841, one ulp below the correctly rounded root
+# 1.3652842 (the float64 root rounded to float32, exact for float32 inputs). The kernel's sqrt is
+# correctly rounded, so the affinity planes can differ from the reference's by that ulp.
+SQRT_X_BITS = 0x3FEE9794
+
+
+def _f32(bits):
+    return np.array([bits], dtype=np.uint32).view(np.float32)
+
+
+def test_torch_cpu_sqrt_within_one_ulp_below():
+    x = _f32(SQRT_X_BITS)
+    cr = np.sqrt(x.astype(np.float64)).astype(np.float32)
+    assert cr.view(np.uint32)[0] == 0x3FAEC1A2  # 1.3652842
+    got = torch.sqrt(torch.from_numpy(x)).numpy()
+    # correctly rounded, or (MKL VML) exactly one ulp below — never above, never further
+    assert int(cr.view(np.int32)[0]) - int(got.view(np.int32)[0]) in (0, 1)
+    # the same bound over a million uniform samples in [0, 2): the tolerance's premise
+    xs = (torch.rand(1 << 20, generator=torch.Generator().manual_seed(0)) * 2).numpy()
+    d = np.sqrt(xs.astype(np.float64)).astype(np.float32).view(np.int32).astype(np.int64) - \
+        torch.sqrt(torch.from_numpy(xs)).numpy().view(np.int32).astype(np.int64)
+    assert d.min() >= 0 and d.max() <= 1
+
+
+def test_targets_reject_inconsistent_out_shape():
+    """The kernels derive out_h / out_w from in_h // downsample_ratio: a config that disagrees is
+    refused before anything is launched (a duck-typed config would otherwise be written OOB)."""
+    from tauv_vision_amd import loss as L
+    mc = types.SimpleNamespace(in_h=64, in_w=96, downsample_ratio=4, out_h=16, out_w=25)
+    tc = types.SimpleNamespace(keypoint_heatmap_sigma=2.0, keypoint_affinity_sigma=3.0)
+    oc = types.SimpleNamespace(n_labels=2, n_keypoints=2)
+    truth = types.SimpleNamespace(valid=torch.zeros(1, 0, dtype=torch.bool))
+    with pytest.raises(ValueError, match="out_h/out_w"):
+        L.generate_heatmap(truth, mc, tc, oc)
+    with pytest.raises(ValueError, match="out_h/out_w"):
+        L.generate_keypoint_heatmap(truth, mc, tc, oc)
+
+
 @pytest.mark.gpu
 def test_gpu_targets_empty_and_all_invalid():
     from tauv_vision_amd import loss as L

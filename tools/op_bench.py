@@ -1,5 +1,5 @@
 """Per-op HIP-event times of the bench workload (B=64 u8 frames, R18 640x480) for A/B runs of
-engine env switches (TV_STEM, TV_STEM_ABLATE, ...): prints the ops whose label matches --match.
+engine knobs (TV_STEM, TV_CONVT, ... — the names engine.cpp accepts): prints the ops whose label matches --match.
 Usage: python tools/op_bench.py [--match projection_layer] [--reps 5] [--precision fp16]"""
 import argparse
 import os

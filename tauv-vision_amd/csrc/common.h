@@ -188,6 +188,26 @@ size_t stem_weight_bytes();
 void stem_fragment_order(const uint16_t* w, int Npad, int Kpad, uint16_t* out);
 int launch_stem(const StemParams& p, int dtype, int grid, hipStream_t s);
 
+// Fused staging + 7x7 stem + ResidualBlock conv1 (3x3 / stride 2) (stem_s2.hip), fp16/bf16, 128
+// channels: writes conv1's activations and the stem at the even pixels (the block's residual input)
+struct StemS2Params {
+  const void* input;      // u8 NHWC [B,H,W,3] frames (u8 = 1) or normalised fp32 NCHW [B,3,H,W]
+  int u8;
+  int B, H, W, Ho, Wo;    // Ho = ceil(H / 2), Wo = ceil(W / 2)
+  const void* stem_w;     // stem_weight_bytes() in B-fragment order (stem_fragment_order), 128 channels
+  const float* stem_bias; // [128] fp32, BN folded
+  const void* w1;         // stem_s2_weight_bytes(): conv1 weights in the kernel's k-step order (stem_s2_repack)
+  const float* bias1;     // [128] fp32, BN folded
+  void* out;              // conv1 + BN + ReLU, NHWC [B,Ho,Wo,out_ldc]
+  int out_ldc;
+  void* res;              // stem(2y, 2x), NHWC [B,Ho,Wo,res_ldc]
+  int res_ldc;
+};
+int stem_s2_tiles(int B, int Ho, int Wo);
+size_t stem_s2_weight_bytes();
+int stem_s2_repack(const void* w, int Kpad, int esz, void* out, hipStream_t s);
+int launch_stem_s2(const StemS2Params& p, int dtype, int cu_count, hipStream_t s);
+
 // ConvTranspose2d(k = s) + pad_to_match + skip add (convt.hip), fp16/bf16, 128 -> 128 channels.
 struct ConvTParams {
   const void* src;    // low-res input NHWC [B,h,w,*]

@@ -303,6 +303,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_C3_TW") c3_tw_force = v == 16 ? 16 : v == 32 ? 32 : 0;
     else if (k == "TV_CUS") cu_count = std::max(8, std::min(cu_count, v));
     else if (k == "TV_STEM") stem_mode = v;
+    else if (k == "TV_STEMFUSE") stemfuse_mode = v;
     else if (k == "TV_LAT") lat_mode = v;
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
@@ -358,6 +359,40 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
         stem_op = (int)i + 1;
         break;
       }
+  // stem + block0.conv1 in one launch (stem_s2.hip): the 128-channel stem feeds exactly the block's
+  // stride-2 3x3 conv1 and its stride-2 1x1 conv_residual (dla.py:13-37, 182-186). The plan gets a
+  // tensor R = stem(2y, 2x) [Ho, Wo, 128], written by the fused launch (conv1's second output) and
+  // read by conv2's residual segment at stride 1; the stem output itself is never stored.
+  if (stemfuse_mode && stem_op >= 0 && stem_op + 2 < (int)plan.ops.size()) {
+    const OpSpec& st = plan.ops[stem_op];
+    const OpSpec& c1 = plan.ops[stem_op + 1];
+    const OpSpec& c2 = plan.ops[stem_op + 2];
+    const int so = st.out;
+    bool ok = st.N == 128 && so >= 0 && plan.tensors[so].C == 128 && c1.kind == OP_CONV && c1.segs.size() == 1 &&
+              c1.segs[0].src == so && c1.segs[0].kh == 3 && c1.segs[0].kw == 3 && c1.segs[0].stride == 2 &&
+              c1.segs[0].pad == 1 && (c1.segs[0].pad_w < 0 || c1.segs[0].pad_w == 1) && !c1.segs[0].row_expand &&
+              c1.segs[0].ci0 == 0 && c1.segs[0].cin == 128 && c1.N == 128 && c1.act == 1 && c1.out >= 0 &&
+              c1.add < 0 && !c1.up_s && c1.stack_w.empty() && plan.tensors[c1.out].C == 128 &&
+              plan.tensors[c1.out].H == (desc.in_h + 1) / 2 && plan.tensors[c1.out].W == (desc.in_w + 1) / 2 &&
+              c2.kind == OP_CONV && c2.segs.size() == 2 && c2.segs[0].src == c1.out && c2.segs[1].src == so &&
+              c2.segs[1].kh == 1 && c2.segs[1].kw == 1 && c2.segs[1].stride == 2 && c2.segs[1].pad == 0 &&
+              !c2.segs[1].identity && c2.segs[1].ci0 == 0 && c2.segs[1].cin == 128;
+    for (size_t i = 0; ok && i < plan.ops.size(); ++i) {  // nothing else reads the stem output
+      if ((int)i == stem_op + 1 || (int)i == stem_op + 2) continue;
+      const OpSpec& o = plan.ops[i];
+      ok = o.src != so && o.add != so;
+      for (const SegSpec& sg : o.segs) ok = ok && sg.src != so;
+    }
+    if (ok) {
+      const TensorSpec t1 = plan.tensors[c1.out];
+      plan.tensors.push_back(TensorSpec{t1.H, t1.W, 128});
+      const int r = (int)plan.tensors.size() - 1;
+      plan.ops[stem_op + 1].out2 = r;
+      plan.ops[stem_op + 2].segs[1].src = r;
+      plan.ops[stem_op + 2].segs[1].stride = 1;
+      ss2_op = stem_op + 1;
+    }
+  }
   packed.resize(plan.ops.size());
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     rc = pack_op(i);
@@ -374,6 +409,7 @@ Engine::~Engine() {
     if (p.w_c3) (void)hipFree(p.w_c3);
     if (p.w_c3h) (void)hipFree(p.w_c3h);
     if (p.w_c3e) (void)hipFree(p.w_c3e);
+    if (p.w_ss2) (void)hipFree(p.w_ss2);
     if (p.head_w) (void)hipFree(p.head_w);
     if (p.head_b) (void)hipFree(p.head_b);
     if (p.bias) (void)hipFree(p.bias);
@@ -402,6 +438,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (op.out >= 0) def[op.out] = (int)i, last[op.out] = std::max(last[op.out], (int)i);
+    if (op.out2 >= 0) def[op.out2] = (int)i, last[op.out2] = std::max(last[op.out2], (int)i);
     for (const SegSpec& s : op.segs) last[s.src] = std::max(last[s.src], (int)i);
     if (op.src >= 0) last[op.src] = std::max(last[op.src], (int)i);
     if (op.add >= 0) last[op.add] = std::max(last[op.add], (int)i);
@@ -439,20 +476,25 @@ int Engine::make_workspace(int B, Workspace* ws) {
     const OpSpec& op = plan.ops[i];
     live.erase(std::remove_if(live.begin(), live.end(), [&](const Live& l) { return l.last < (int)i; }), live.end());
     if (op.out < 0 || (stem_op >= 0 && op.kind == OP_PREP)) continue;  // fused stem: no staged input
+    if (ss2_op >= 0 && (int)i == stem_op) continue;                      // stem fused into block0.conv1: never stored
     if (virt[op.out]) continue;                                          // fused DCN: no column tensor
-    if (placed[op.out]) continue;
-    placed[op.out] = 1;
-    const TensorSpec& t = plan.tensors[op.out];
-    size_t sz = align_up((size_t)B * t.H * t.W * t.C * esz, 256);
-    std::sort(live.begin(), live.end(), [](const Live& a, const Live& b) { return a.off < b.off; });
-    size_t pos = 0;
-    for (const Live& l : live) {
-      if (pos + sz <= l.off) break;
-      pos = std::max(pos, l.off + l.size);
-    }
-    ws->off[op.out] = pos;
-    live.push_back({pos, sz, last[op.out]});
-    peak = std::max(peak, pos + sz);
+    auto place = [&](int tid) {
+      if (placed[tid]) return;
+      placed[tid] = 1;
+      const TensorSpec& t = plan.tensors[tid];
+      size_t sz = align_up((size_t)B * t.H * t.W * t.C * esz, 256);
+      std::sort(live.begin(), live.end(), [](const Live& a, const Live& b) { return a.off < b.off; });
+      size_t pos = 0;
+      for (const Live& l : live) {
+        if (pos + sz <= l.off) break;
+        pos = std::max(pos, l.off + l.size);
+      }
+      ws->off[tid] = pos;
+      live.push_back({pos, sz, last[tid]});
+      peak = std::max(peak, pos + sz);
+    };
+    place(op.out);
+    if (op.out2 >= 0) place(op.out2);
   }
   ws->bytes = peak;
   ws->B = B;
@@ -593,7 +635,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
                       (size_t)p.seg[1].H * p.seg[1].W * p.seg[1].ldc * esz < (1ull << 31) &&
                       p.seg[1].H >= (p.Ho - 1) * p.seg[1].stride + 1 && p.seg[1].W >= (p.Wo - 1) * p.seg[1].stride + 1;
     if (conv3_mode && dtype != F32 && op.kind == OP_CONV && (op.segs.size() == 1 || res2) && op.out >= 0 &&
-        op.add < 0) {
+        op.add < 0 && (int)i != ss2_op) {
       const SegSpec& sg = op.segs[0];
       const ConvSegment& cs = p.seg[0];
       const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
@@ -658,7 +700,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
     }
     // persistent stride-2 3x3 kernel (conv3x3s2.hip): 128 -> 128 channels, fp16/bf16, at least
     // one 512-pixel tile per CU (smaller layers stay on the pipelined implicit GEMM)
-    if (s2_mode && dtype != F32 && op.kind == OP_CONV && op.segs.size() == 1 && op.out >= 0 && op.add < 0) {
+    if (s2_mode && dtype != F32 && op.kind == OP_CONV && op.segs.size() == 1 && op.out >= 0 && op.add < 0 &&
+        (int)i != ss2_op) {
       const SegSpec& sg = op.segs[0];
       const ConvSegment& cs = p.seg[0];
       const int pw = sg.pad_w >= 0 ? sg.pad_w : sg.pad;
@@ -688,7 +731,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (dtype == F32 || op.kind != OP_CONV || op.segs.size() != 1 || op.out < 0 || op.add >= 0 || op.up_s ||
-        ws->c3_tw[i] || ws->s2_grid[i])
+        ws->c3_tw[i] || ws->s2_grid[i] || (int)i == ss2_op)
       continue;
     const SegSpec& sg = op.segs[0];
     const ConvParams& p = ws->params[i];
@@ -798,7 +841,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
   for (size_t i = 0; lat_mode && dtype != F32 && i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     ConvParams& p = ws->params[i];
-    if (op.kind != OP_CONV || op.up_s || op.out < 0 || op.add >= 0 || (int)i == stem_op || op_ks[i].empty() ||
+    if (op.kind != OP_CONV || op.up_s || op.out < 0 || op.add >= 0 || (int)i == stem_op || (int)i == ss2_op ||
+        op_ks[i].empty() ||
         ws->small[i] || ws->dcn[i].x || ws->dcn_skip[i] || ws->head_fused[i] || ws->head_skip[i] || p.N % 8 ||
         p.out_ldc % 8 || p.out_coff % 8)
       continue;
@@ -858,6 +902,16 @@ int Engine::make_workspace(int B, Workspace* ws) {
     }
   }
   if (stamp_op >= 0 && stamp_op < (int)plan.ops.size() && ws->c3_tw[stamp_op]) ws->params[stamp_op].dbg = stamp_buf;
+  if (ss2_op >= 0) {  // block0.conv1 fused with the stem: its weights in stem_s2.hip's k-step order
+    ws->use_pipe[ss2_op] = 0;
+    Packed& pk = packed[ss2_op];
+    if (!pk.w_ss2) {
+      TV_HIP(hipMalloc(&pk.w_ss2, stem_s2_weight_bytes()));
+      int rc = stem_s2_repack(pk.w, pk.Kpad, esz, pk.w_ss2, nullptr);
+      if (rc) return rc;
+      TV_HIP(hipDeviceSynchronize());
+    }
+  }
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
@@ -913,6 +967,29 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const OpSpec& op = plan.ops[i];
   char* base = (char*)ws->arena;
   if (stem_op >= 0 && op.kind == OP_PREP) return TV_OK;  // staging runs inside the stem kernel
+  if (ss2_op >= 0 && (int)i == stem_op) return TV_OK;    // the stem runs inside block0.conv1's launch
+  if ((int)i == ss2_op) {
+    const OpSpec& st = plan.ops[stem_op];
+    const TensorSpec& t1 = plan.tensors[op.out];
+    StemS2Params sp{};
+    sp.input = input;
+    sp.u8 = input_u8;
+    sp.B = ws->B;
+    sp.H = desc.in_h;
+    sp.W = desc.in_w;
+    sp.Ho = t1.H;
+    sp.Wo = t1.W;
+    sp.stem_w = packed[stem_op].w;
+    sp.stem_bias = packed[stem_op].bias;
+    (void)st;
+    sp.w1 = packed[i].w_ss2;
+    sp.bias1 = packed[i].bias;
+    sp.out = base + ws->off[op.out];
+    sp.out_ldc = t1.C;
+    sp.res = base + ws->off[op.out2];
+    sp.res_ldc = plan.tensors[op.out2].C;
+    return launch_stem_s2(sp, dtype, cu_count, s);
+  }
   if ((int)i == stem_op) {
     StemParams sp{};
     sp.input = input;
@@ -1100,6 +1177,13 @@ const char* Engine::op_kernel(int B, size_t i) {
     static const char* tn[3] = {"float", "_Float16", "__bf16"};
     const OpSpec& op = plan.ops[i];
     if (op.kind == OP_PREP) return stem_op >= 0 ? "prep (fused into the stem)" : "prep";
+    if (ss2_op >= 0 && (int)i == stem_op) return "(fused into block_layers.0.conv1: stem_s2)";
+    if ((int)i == ss2_op) {
+      std::string& name = ws->kname[i];  // (input kind of the last profile(): rebuilt per call)
+      const int smode = profiled_u8 ? (desc.in_w % 4 == 0 ? 2 : 1) : 0;
+      name = std::string("tv::ss2::stem_s2<") + tn[dtype] + ", " + std::to_string(smode) + ">";
+      return name.c_str();
+    }
     if ((int)i == stem_op) {
       std::string& name = ws->kname[i];  // (input kind of the last profile(): rebuilt per call)
       const int smode = profiled_u8 ? (desc.in_w % 4 == 0 ? 2 : 1) : 0;

@@ -16,6 +16,7 @@ struct Packed {
   void* w_c3 = nullptr;    // conv3x3.hip / conv3x3s2.hip k-step-major copy (made on first use)
   void* w_c3h = nullptr;   // conv3x3.hip copy for 64-channel half tiles (ni = 2)
   void* w_c3e = nullptr;   // conv3x3.hip copy for the fused-heads body when its swizzle differs (conv3x3_k16)
+  void* w_ss2 = nullptr;   // stem_s2.hip k-step-ordered copy of block0.conv1's weights (made on first use)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;
@@ -86,6 +87,9 @@ struct Engine {
   unsigned long long* stamp_buf = nullptr;
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)
   int stem_op = -1;            // op index of the 7x7 stem conv when it runs on stem.hip, else -1
+  int stemfuse_mode = 1;       // stem + block0.conv1 (+ the residual's stride-2 stem samples) in one launch
+                               // (stem_s2.hip) when the plan has that shape (knob TV_STEMFUSE=0 off)
+  int ss2_op = -1;             // op index of block0.conv1 when it runs fused with the stem, else -1
   // concurrent slices: a batch of >= slices * slice_min frames runs as `slices` near-equal parts,
   // the first on the caller's stream and the others on side streams (fork / join events), so one
   // slice's latency-bound small layers and grid tails overlap another's large layers

@@ -69,6 +69,9 @@ struct OpSpec {
   // OP_CONV with up_s > 0: a phase-scatter GEMM over the (gh, gw) grid of its input whose output
   // pixel (oy, ox) lands at (oy * up_s + sy, ox * up_s + sx) of `out` (no skip tensor when add < 0)
   int gh = 0, gw = 0;
+  // a second output tensor (the fused stem + block0.conv1 launch also writes the stem at the even
+  // pixels, the block's residual input): placed and kept live like `out`
+  int out2 = -1;
 };
 
 struct TensorSpec {

@@ -8,51 +8,64 @@
 // Why: unfused, the stem writes 128 channels x 2 B per input pixel (5.0 GB per 64-frame batch)
 // and conv1 + the residual read them back (~10 GB of fetches with halo re-reads): the largest
 // avoidable HBM round trip of the R18 step. Here the stem output never reaches HBM:
-//  * a persistent 512-thread workgroup per CU owns 16 x 32-pixel conv1 output tiles; per tile
-//    the conv1 K loop is 36 k-steps (9 taps x 4 channel blocks of 32) as in conv3x3s2.hip —
-//    virtual space-to-depth: for each (input row parity p, column parity q) phase block the
-//    taps read a (16 + p) x (32 + q) halo of stem pixels (2(oy0 - p + hy) + p, 2(ox0 - q + hx) + q)
-//    at 80-byte pitch with compile-time immediate ds_read offsets;
-//  * the halo of one (phase block, channel block) is not loaded: it is COMPUTED into LDS by the
-//    same waves right before its 1-4 k-steps (stem phase: 7x7 conv of the phase block's pixels
-//    for the 32 channels, 32x32x16 MFMAs, K = 7 rows x 24 = 168 of the row-expanded input E,
-//    bias + ReLU, zeros outside the image = conv1's padding);
-//  * the block order (q = 1 first, then q = 0; per channel block the p = 0 block first) lets the
-//    expanded input E hold one column parity at a time (39 rows x 33 pixels x 48 B) and lets the
-//    next channel block's stem weights (44 VGPRs) load under the longer p = 1 block's k-steps;
-//  * the input window of the next tile (39 x 71 pixels, u8 HWC through the 768-entry LUT or
-//    normalised fp32 NCHW) is fetched into registers in the middle of the current tile;
+//  * a persistent 512-thread workgroup per CU (8 waves, two per SIMD) owns 16 x 32 conv1 output
+//    tiles; wave w computes rows 2w, 2w + 1 x all 128 channels (8 32x32 MFMA accumulators, 8
+//    MFMAs per 16-deep sub-step on 6 fragment reads). Measured alternatives (profiles/r4): 8 x 32
+//    tiles (64 x 64 per wave) 1.41-1.47 ms per 32-frame slice, the per-k-step overhead on half
+//    the MFMAs; one 512-register wave per SIMD (4 waves, 128 x 128 each) 1.94 ms; this form
+//    1.19-1.22 ms against 1.30 for stem.hip + conv3x3s2.hip;
+//  * conv1's K loop is 36 k-steps (9 taps x 4 channel blocks of 32), as in conv3x3s2.hip —
+//    virtual space-to-depth: for each (input row parity p, column parity q) phase block the taps
+//    read a (16 + p) x (32 + q) halo of stem pixels (2(oy0 - p + hy) + p, 2(ox0 - q + hx) + q) at
+//    80-byte pitch with compile-time immediate ds_read offsets; weights register-staged five
+//    k-steps ahead into a 3-slot LDS ring, one barrier per k-step;
+//  * the halo of one (phase block, channel block) is not loaded: it is COMPUTED into LDS right
+//    before its 1-4 k-steps (stem phase: the 7x7 conv of the block's pixels for its 32 channels,
+//    32x32x16 MFMAs in pairs of independent fragments, K = 7 rows x 24 = 168 of the row-expanded
+//    input E, bias + ReLU, zeros outside the image = conv1's padding; one fragment per wave at a
+//    time: the SIMD's two waves interleave their dependent accumulation chains);
+//  * the block order (q = 1 then q = 0; per channel block p = 0 then p = 1) lets E hold one
+//    column parity at a time (39 rows x 33 pixels x 48 B) and lets the next channel block's stem
+//    weights (44 VGPRs, A operands) load under the longer p = 1 block's k-steps;
+//  * the next tile's input window (39 x 71 pixels of u8 HWC, 5 dwords per thread) is fetched into
+//    registers in the middle of the current tile and normalised through the 768-entry LUT; the
+//    other inputs (normalised fp32 NCHW, u8 of a width not a multiple of 4: 17 values per
+//    thread) load at the tile's start, which keeps the kernel inside 256 VGPRs;
 //  * the (0, 0) phase block of each channel block IS the stem at the even pixels: it is copied
 //    from LDS to `res` (the residual input, [B, Ho, Wo, 128]), which conv2's fused 1x1 residual
 //    then reads at stride 1 instead of the 128 x 480 x 640 stem tensor at stride 2.
-// Every vector-memory operation in the tile body is issued unconditionally (out-of-range lanes
+// Every vector-memory operation of the tile body is issued unconditionally (out-of-range lanes
 // use out-of-range buffer offsets), so the compiler's counted waits for the weight ring are exact.
 // LDS: halo 44,880 + E 61,776 + window 17,472 + conv1 weight ring 24,576 + biases + LUT = 151,264 B.
+// Numerics: the stem values are rounded to the compute dtype exactly as stem.hip stores them;
+// conv1 accumulates the same products in fp32 in another k-step order than conv3x3s2.hip.
 #include "conv_common.h"
 
 #include <type_traits>
 
 #ifndef TV_SS2_EXP
-#define TV_SS2_EXP 0  // timing-only diagnostic builds (wrong results): 1 = no stem MFMAs, 2 = no conv1 MFMAs
+#define TV_SS2_EXP 0  // timing-only diagnostic builds (wrong results): 1 = no stem MFMAs
 #endif
 
 namespace tv {
 namespace ss2 {
 
-constexpr int NT = 512, BN = 128, TH = 8, TW = 32;
+constexpr int NT = 512, NWV = 8, BN = 128, TH = 16, TW = 32;
+constexpr int RPW = TH / NWV;                     // output rows (32-pixel fragments) per wave
 constexpr int RS = TW + 1;                        // halo row stride (pixels)
 constexpr int PITCH = 80;                         // halo pixel pitch (bytes): 32 channels + pad
 constexpr int HBYTES = (TH + 1) * RS * PITCH;     // one (phase block, channel block) halo
-constexpr int WR = 2 * TH + 7, WCOL = 2 * TW + 7; // input window rows / pixels (23 x 71)
+constexpr int WR = 2 * TH + 7, WCOL = 2 * TW + 7; // input window rows / pixels (39 x 71)
 constexpr int NVROW = WCOL * 3;                   // values per window row (213)
 constexpr int NPITCH = 448;                       // bytes per normalised window row in LDS
 constexpr int EPIX = 48, ECOLS = RS;              // row-expanded operand: 24 values per (row, pixel)
 constexpr int EBYTES = WR * ECOLS * EPIX;
 constexpr int KS = 11;                            // stem MFMA k-steps (K = 176 >= 168)
 constexpr int WSLOT = BN * 64;                    // conv1 weights of one k-step
+constexpr int WPL = WSLOT / NT;                   // weight bytes per lane per k-step (16)
 constexpr int RING = 3;
-constexpr int OFF_H = 0;                          // two halo buffers: block b reads H[b & 1] while the
-constexpr int OFF_E = OFF_H + 2 * HBYTES;         // next block's stem is computed into the other
+constexpr int OFF_H = 0;
+constexpr int OFF_E = OFF_H + HBYTES;
 constexpr int OFF_N = OFF_E + EBYTES;
 constexpr int OFF_W = OFF_N + WR * NPITCH;
 constexpr int OFF_B1 = OFF_W + RING * WSLOT;
@@ -63,6 +76,7 @@ static_assert(LDS <= 160 * 1024, "LDS budget");
 static_assert(OFF_E % 16 == 0 && OFF_N % 16 == 0 && OFF_W % 16 == 0 && OFF_B1 % 16 == 0 && OFF_LUT % 16 == 0,
               "16-byte aligned carve");
 static_assert(NPITCH >= NVROW * 2 + 20, "expand reads 5 dwords past a chunk start");
+static_assert(WPL == 16, "one 16-byte weight chunk per lane per k-step");
 
 // ---- block / k-step schedule of a tile: block b = (column parity q, channel block cb, row
 // parity p): q = 1 for b < 8; cb = (b & 7) / 2; p = b & 1
@@ -95,14 +109,6 @@ constexpr Sched make_sched() {
   return sc;
 }
 constexpr Sched SCH = make_sched();
-// k-step (within block b) at which fragment ordinal n of block b + 1's stem is computed: an odd
-// block waits one k-step (its first) for the stem weights of the new channel block / E's q = 0
-// copy (block 7); a 1-k-step block does both ordinals in it
-constexpr int stem_slot(int b, int n) {
-  const int L = pb_len(blk_p(b), blk_q(b));
-  const int t = (b & 1) ? n + 1 : n;
-  return t < L ? t : L - 1;
-}
 static_assert(SCH.first[NBLK - 1] + pb_len(1, 0) == SPT, "36 k-steps per tile");
 
 template <int MODE> struct Win;  // input window staging: registers per thread
@@ -155,14 +161,17 @@ __device__ __forceinline__ unsigned pack2(float a, float b) {
   return __builtin_bit_cast(unsigned, t2{(T)a, (T)b});
 }
 
-struct Half {  // conv1 fragments of one 16-deep sub-step
-  u32x4 x[2];  // pixel fragments (tile rows 2 (w % 4), + 1)
-  u32x4 w[2];  // channel fragments (channels 64 (w / 4) + 32 i)
+struct Half {     // conv1 fragments of one 16-deep sub-step
+  u32x4 x[RPW];   // pixel fragments: tile rows 4w + f
+  u32x4 w[4];     // channel fragments: channels 32 i
+};
+struct WReg {
+  u32x4 a;
 };
 
-// a lane value the compiler must recompute where it is used: keeps the per-block stem / copy
-// addresses (functions of the lane alone) from being hoisted out of the tile loop, where 16
-// blocks' worth of them would stay live across the whole tile and spill
+// a lane value the compiler must recompute where it is used: keeps the per-block stem / copy /
+// staging addresses (functions of the lane alone) from being hoisted out of the tile loop, where
+// 16 blocks' worth of them would stay live across the whole tile
 __device__ __forceinline__ int opaque(int v) {
   asm volatile("" : "+v"(v));
   return v;
@@ -282,7 +291,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       }
     }
   };
-  // N -> E for column parity Q: E[r][hx] = the 24 values from window pixel c0 = 2 hx - Q + 1 on
+  // N -> E for column parity Q: E[r][hx] = the 24 values from window pixel 2 hx - Q + 1 on
   // (7 horizontal taps x 3 channels of stem column 2 ox0 + 2 hx - Q; values 21..23 zero)
   auto expand = [&](auto qc) __attribute__((always_inline)) {
     constexpr int Q = decltype(qc)::value, NC = TW + Q, TOT = WR * NC * 3;
@@ -309,8 +318,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   // ---- stem weights of one channel block: A-fragments (32 channels x 16 K per k-step), one
-  // 16-byte global load per k-step per lane (stem_fragment_order; L2-resident)
-  // (through a buffer resource: one lane-offset VGPR, the fragment offset in an SGPR)
+  // 16-byte load per k-step per lane (stem_fragment_order; L2-resident), through a buffer resource
   uint4 wst[KS];
   const i32x4 srsrc = rsrc_of(p.stem_w, (unsigned long long)KS * 4 * 1024);
   auto load_stem_w = [&](int cb) __attribute__((always_inline)) {
@@ -320,19 +328,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 
   // ---- stem phase: the halo of phase block (P, Q), channel block CB of tile (oy0, ox0) into LDS.
   // Fragment k = 32 consecutive pixels of the (16 + P) x (32 + Q) block (row-major); wave w
-  // computes fragments w, w + 8, ...; lane (l32, lh): pixel l32, K half lh.
-  auto stem_frag = [&](auto bc, auto nc, int oy0, int ox0) __attribute__((always_inline)) {
-    constexpr int B = decltype(bc)::value, NO = decltype(nc)::value;
+  // computes fragments w, w + 4, ... two at a time (independent accumulators keep the one wave
+  // of the SIMD issuing back to back); lane (l32, lh): pixel l32, K half lh.
+  auto stem_phase = [&](auto bc, int oy0, int ox0) __attribute__((always_inline)) {
+    constexpr int B = decltype(bc)::value;
     constexpr int P = blk_p(B), Q = blk_q(B), CB = blk_cb(B);
     constexpr int NC = TW + Q, NPX = (TH + P) * NC, NFR = (NPX + 31) / 32;
-    static_assert(NFR <= 16, "two fragment ordinals per wave");
     const float* lbs = reinterpret_cast<const float*>(smem + OFF_BS) + CB * 32;
-    const int k = wave + 8 * NO;
-    if (k < NFR) {  // wave-uniform
-      int f = 32 * k + opaque(l32);
-      const bool valid = f < NPX;
-      f = valid ? f : NPX - 1;
-      const int hy = f / NC, hx = f - hy * NC;
+    for (int k = wave; k < NFR; k += NWV) {  // (wave-uniform trip count; the SIMD's two waves interleave)
+      int ff = 32 * k + opaque(l32);
+      const bool valid = ff < NPX;
+      ff = valid ? ff : NPX - 1;
+      const int hy = ff / NC, hx = ff - hy * NC;
       const char* e0 = smem + OFF_E + ((2 * hy - P + 1) * ECOLS + hx) * EPIX;
       const char* e16 = e0 + lh * 16;
       const char* erow = e0 + lh * (ECOLS * EPIX - 32);
@@ -351,7 +358,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       }
       const int sy = 2 * oy0 + 2 * hy - P, sx = 2 * ox0 + 2 * hx - Q;
       const bool in = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
-      char* hdst = smem + OFF_H + (B & 1) * HBYTES + (hy * RS + hx) * PITCH;
+      char* hdst = smem + OFF_H + (hy * RS + hx) * PITCH;
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         float v[2][4];
@@ -374,47 +381,43 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // ---- conv1: register-staged weight ring (conv3x3s2.hip): k-step q loaded at step q - 5 into
   // set q % 4, written to ring slot q % 3 at step q - 2; [k-step][128 rows][4 x 16 B] (stem_s2_repack)
   int wc_in = 0;
-  u32x4 wreg[4];
+  WReg wreg[4];
   const i32x4 wrsrc = rsrc_of(p.w1, (unsigned long long)SPT * WSLOT);
-  const int wvoff = wave * 1024 + lane * 16;
-  auto w_load = [&](u32x4& dst) __attribute__((always_inline)) {
-    dst = raw_buffer_load_v4(wrsrc, wvoff, wc_in * WSLOT, 0);
+  const int wvoff = tid * WPL;
+  auto w_load = [&](WReg& dst) __attribute__((always_inline)) {
+    dst.a = raw_buffer_load_v4(wrsrc, wvoff, wc_in * WSLOT, 0);
     if (++wc_in == SPT) wc_in = 0;
   };
+  auto w_store = [&](int slot, const WReg& v) __attribute__((always_inline)) {
+    *reinterpret_cast<u32x4*>(smem + OFF_W + slot * WSLOT + wvoff) = v.a;
+  };
   const unsigned lds0 = (unsigned)(uintptr_t)smem;
-  // wave w: tile rows 2 (w % 4) + f (f = 0, 1) x output channels 64 (w / 4) + 32 i (i = 0, 1)
-  const int wrow = 2 * (wave & 3), wch = 64 * (wave >> 2);
-  const unsigned xa = lds0 + OFF_H + (unsigned)((wrow * RS + l32) * PITCH + lh * 16);  // row 2(w % 4), col l32
+  // wave w: tile rows RPW w + f (f = 0..3) x all 128 output channels (fragments i = 0..3)
+  const unsigned xa = lds0 + OFF_H + (unsigned)((RPW * wave * RS + l32) * PITCH + lh * 16);
   constexpr int FOFF = RS * PITCH;
   unsigned wa[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-    wa[j] = lds0 + OFF_W + (unsigned)((wch + l32) * 64 + (((2 * j + lh) ^ ((l32 >> 2) & 3)) << 4));
-  auto read_one = [&](auto r, auto sj, auto kj, auto hb, unsigned xb, unsigned wb, Half& F) __attribute__((always_inline)) {
+  for (int j = 0; j < 2; ++j) wa[j] = lds0 + OFF_W + (unsigned)(l32 * 64 + (((2 * j + lh) ^ ((l32 >> 2) & 3)) << 4));
+  // fragment R of sub-step SJ of k-step j: x[R] for R < RPW, else w[R - RPW]
+  auto read_one = [&](auto r, auto sj, auto kj, unsigned xb, unsigned wb, Half& F) __attribute__((always_inline)) {
     constexpr int R = decltype(r)::value, SJ = decltype(sj)::value, KJ = decltype(kj)::value;
-    constexpr int TOFF = (J_TY[KJ] * RS + J_TX[KJ]) * PITCH + decltype(hb)::value * HBYTES;
-    if constexpr (R < 2) F.x[R] = ds_read16<TOFF + 32 * SJ + R * FOFF>(xb);
-    else F.w[R - 2] = ds_read16<(R - 2) * 2048>(wb);
+    constexpr int TOFF = (J_TY[KJ] * RS + J_TX[KJ]) * PITCH;
+    if constexpr (R < RPW) F.x[R] = ds_read16<TOFF + 32 * SJ + R * FOFF>(xb);
+    else F.w[R - RPW] = ds_read16<(R - RPW) * 2048>(wb);
   };
-  f32x16 acc[2][2];
-  auto mfma_pair = [&](auto i, auto firstc, const Half& F) __attribute__((always_inline)) {
+  f32x16 acc[RPW][4];
+  // the RPW MFMAs of channel fragment I (all pixel fragments)
+  auto mfma_col = [&](auto i, auto firstc, const Half& F) __attribute__((always_inline)) {
     constexpr int I = decltype(i)::value;
-    if constexpr (decltype(firstc)::value) {
-      acc[0][I] = f32x16{};
-      acc[1][I] = f32x16{};
+#pragma unroll
+    for (int f = 0; f < RPW; ++f) {
+      if constexpr (decltype(firstc)::value) acc[f][I] = f32x16{};
+      Mfma<T>::run(to_u4(F.w[I]), to_u4(F.x[f]), acc[f][I]);
     }
-#if TV_SS2_EXP == 2
-    acc[0][I][0] += __uint_as_float(F.w[I].x ^ F.x[0].x);
-    acc[1][I][0] += __uint_as_float(F.w[I].y ^ F.x[1].y);
-#else
-    Mfma<T>::run(to_u4(F.w[I]), to_u4(F.x[0]), acc[0][I]);
-    Mfma<T>::run(to_u4(F.w[I]), to_u4(F.x[1]), acc[1][I]);
-#endif
   };
 
   // residual input: the (0, 0) phase block of channel block CB = stem(2 (oy0 + hy), 2 (ox0 + hx))
-  // for the tile's 8 x 32 output pixels, LDS -> res (2 chunks of 16 B per thread); the (0, 0)
-  // blocks are the even ones (p = b & 1 = 0), in halo buffer 0
+  // for the tile's 16 x 32 output pixels, LDS -> res (8 chunks of 16 B per thread)
   const unsigned long long res_frame = (unsigned long long)Ho * Wo * p.res_ldc * sizeof(T);
   auto copy_res = [&](auto cbc, int fr, int oy0, int ox0) __attribute__((always_inline)) {
     constexpr int CB = decltype(cbc)::value;
@@ -434,7 +437,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   Half H0, H1;
-  int cur_fr = 0, cur_y0 = 0, cur_x0 = 0, tl_cur = 0;
+  int cur_fr = 0, cur_y0 = 0, cur_x0 = 0;
   // one conv1 k-step at schedule position QS of the tile (block SCH.blk, tap j)
   auto step = [&](auto qc) __attribute__((always_inline)) {
     constexpr int QS = decltype(qc)::value;
@@ -450,52 +453,53 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const unsigned wc1 = wa[1] + (unsigned)(SLOT * WSLOT);
     const unsigned wn0 = wa[0] + (unsigned)(((QS + 1) % RING) * WSLOT);
     if constexpr (FIRSTK) {  // the block's first k-step: its sub-step-0 fragments were not read ahead
-      read_one(IC<0>{}, IC<0>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc0, H0);
-      read_one(IC<1>{}, IC<0>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc0, H0);
-      read_one(IC<2>{}, IC<0>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc0, H0);
-      read_one(IC<3>{}, IC<0>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc0, H0);
+      auto rd = [&](auto r) __attribute__((always_inline)) { read_one(r, IC<0>{}, IC<J>{}, xa, wc0, H0); };
+      unroll<0, RPW + 4>(rd);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
-    mfma_pair(IC<0>{}, IC<FIRST>{}, H0);
-    read_one(IC<0>{}, IC<1>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc1, H1);
-    read_one(IC<1>{}, IC<1>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc1, H1);
-    // k-step QS + 2 (loaded at step QS - 3) into the slot k-step QS - 1 used (read before this barrier)
-    *reinterpret_cast<u32x4*>(smem + OFF_W + ((QS + 2) % RING) * WSLOT + wave * 1024 + lane * 16) = wreg[(PAR + 2) & 3];
+    // first half: sub-step 0 (H0) MFMAs, channel fragment by channel fragment, with sub-step 1's
+    // reads (H1) and the ring write issued between them
+    mfma_col(IC<0>{}, IC<FIRST>{}, H0);
+    read_one(IC<0>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
+    read_one(IC<1>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
     __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<1>{}, IC<FIRST>{}, H0);
-    read_one(IC<2>{}, IC<1>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc1, H1);
-    read_one(IC<3>{}, IC<1>{}, IC<J>{}, IC<BLK & 1>{}, xa, wc1, H1);
+    mfma_col(IC<1>{}, IC<FIRST>{}, H0);
+    read_one(IC<2>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
+    read_one(IC<3>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
+    // k-step QS + 2 (loaded at step QS - 3) into the slot k-step QS - 1 used (read before this barrier)
+    w_store((QS + 2) % RING, wreg[(PAR + 2) & 3]);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_col(IC<2>{}, IC<FIRST>{}, H0);
+    read_one(IC<4>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
+    read_one(IC<5>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
     if constexpr (blk_p(BLK) == 0 && blk_q(BLK) == 0) copy_res(IC<blk_cb(BLK)>{}, cur_fr, cur_y0, cur_x0);
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_col(IC<3>{}, IC<FIRST>{}, H0);
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // H1 landed
     __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<0>{}, IC<false>{}, H1);
+    // second half: sub-step 1 (H1), the next k-step's sub-step-0 reads (within the block) between
+    mfma_col(IC<0>{}, IC<false>{}, H1);
     w_load(wreg[(PAR + 1) & 3]);  // k-step QS + 5 (past the tile's end: the next tile's, same weights)
     if constexpr (!LASTK) {
-      read_one(IC<0>{}, IC<0>{}, IC<J + 1>{}, IC<BLK & 1>{}, xa, wn0, H0);
-      read_one(IC<1>{}, IC<0>{}, IC<J + 1>{}, IC<BLK & 1>{}, xa, wn0, H0);
+      read_one(IC<0>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
+      read_one(IC<1>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    mfma_pair(IC<1>{}, IC<false>{}, H1);
+    mfma_col(IC<1>{}, IC<false>{}, H1);
     if constexpr (!LASTK) {
-      read_one(IC<2>{}, IC<0>{}, IC<J + 1>{}, IC<BLK & 1>{}, xa, wn0, H0);
-      read_one(IC<3>{}, IC<0>{}, IC<J + 1>{}, IC<BLK & 1>{}, xa, wn0, H0);
+      read_one(IC<2>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
+      read_one(IC<3>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // software pipeline: the next block's halo is computed under this block's k-steps
-    if constexpr (BLK == 7 && TB == 0) {
-      expand(IC<0>{});  // E's q = 1 copy was last read by block 7's stem (computed during block 6)
-      int nfr, ny0, nx0;
-      tile_of(tl_cur + 1, nfr, ny0, nx0);
-      load_window(nfr, ny0, nx0);  // the next tile's window, in registers until its store_window
+    mfma_col(IC<2>{}, IC<false>{}, H1);
+    if constexpr (!LASTK) {
+      read_one(IC<4>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
+      read_one(IC<5>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
     }
-    if constexpr (BLK + 1 < NBLK) {
-      if constexpr (stem_slot(BLK, 0) == TB) stem_frag(IC<BLK + 1>{}, IC<0>{}, cur_y0, cur_x0);
-      if constexpr (stem_slot(BLK, 1) == TB) stem_frag(IC<BLK + 1>{}, IC<1>{}, cur_y0, cur_x0);
-    }
-    // the stem weights switch channel block after the last fragment of an odd block's stem
-    if constexpr ((BLK & 1) == 0 && LASTK) load_stem_w(blk_cb((BLK + 2) % NBLK));
+    __builtin_amdgcn_sched_barrier(0);
+    mfma_col(IC<3>{}, IC<false>{}, H1);
     __builtin_amdgcn_sched_barrier(0);
   };
 
@@ -505,19 +509,19 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const float* lb1 = reinterpret_cast<const float*>(smem + OFF_B1);
     const i32x4 ors = rsrc_of((const char*)p.out + (size_t)fr * out_frame, out_frame);
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-      const int y = oy0 + wrow + f, x = ox0 + l32;
+    for (int f = 0; f < RPW; ++f) {
+      const int y = oy0 + RPW * wave + f, x = ox0 + l32;
       const bool ok = y < Ho && x < Wo;
-      const int obase = ok ? (int)(((unsigned)(y * Wo + x) * (unsigned)p.out_ldc + wch + 8 * lh) * sizeof(T)) : OOB;
+      const int obase = ok ? (int)(((unsigned)(y * Wo + x) * (unsigned)p.out_ldc + 8 * lh) * sizeof(T)) : OOB;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < 4; ++i) {
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
           float v[2][4];
 #pragma unroll
           for (int gg = 0; gg < 2; ++gg) {
             const int G2 = 2 * m + gg;
-            const f32x4 bb = *reinterpret_cast<const f32x4*>(lb1 + wch + 32 * i + 8 * G2 + 4 * lh);
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(lb1 + 32 * i + 8 * G2 + 4 * lh);
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[gg][e] = fmaxf(acc[f][i][4 * G2 + e] + bb[e], 0.0f);
           }
@@ -535,20 +539,23 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 
   // ---- prologue: tile 0's window, channel block 0's stem weights, conv1 weights of k-steps 0..4
   tile_of(0, cur_fr, cur_y0, cur_x0);
-  load_window(cur_fr, cur_y0, cur_x0);
+  if constexpr (MODE == 2) load_window(cur_fr, cur_y0, cur_x0);
   load_stem_w(0);
   w_load(wreg[0]);
   w_load(wreg[1]);
-  *reinterpret_cast<u32x4*>(smem + OFF_W + wave * 1024 + lane * 16) = wreg[0];
-  *reinterpret_cast<u32x4*>(smem + OFF_W + WSLOT + wave * 1024 + lane * 16) = wreg[1];
+  w_store(0, wreg[0]);
+  w_store(1, wreg[1]);
   w_load(wreg[2]);
   w_load(wreg[3]);
   w_load(wreg[0]);
-  __syncthreads();  // LUT, biases
+  __syncthreads();  // LUT, biases, ring slots 0 and 1
 
-  // one block: its k-steps (each also computing a part of the next block's stem)
+  // one block: [barrier] stem phase [stem weights of the next channel block] k-steps
   auto block = [&](auto bc) __attribute__((always_inline)) {
     constexpr int B = decltype(bc)::value;
+    lds_barrier();  // the previous block's k-steps have read the halo
+    stem_phase(IC<B>{}, cur_y0, cur_x0);
+    if constexpr (blk_p(B) == 1) load_stem_w(blk_cb((B + 1) % NBLK));  // lands under this block's k-steps
     auto ks = [&](auto t) __attribute__((always_inline)) {
       constexpr int T_ = decltype(t)::value;
       step(IC<SCH.first[B] + T_>{});
@@ -556,18 +563,22 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     unroll<0, pb_len(blk_p(B), blk_q(B))>(ks);
   };
   for (int tl = 0; tl < ntl; ++tl) {
-    tl_cur = tl;
-    // the tile's input window (N, from registers), E for q = 1 and block 0's stem, serially
-    store_window(cur_y0, cur_x0);  // N was last read by expand<0> in block 7 of the previous tile
+    if constexpr (MODE != 2) load_window(cur_fr, cur_y0, cur_x0);
+    store_window(cur_y0, cur_x0);  // N was last read by expand<0> in the previous tile
     lds_barrier();
-    expand(IC<1>{});               // E was last read by the stem of block 15, under block 14
-    lds_barrier();
-    stem_frag(IC<0>{}, IC<0>{}, cur_y0, cur_x0);  // into H[0], last read by block 14's k-steps
-    stem_frag(IC<0>{}, IC<1>{}, cur_y0, cur_x0);
-    unroll<0, NBLK>(block);
+    expand(IC<1>{});               // E was last read by block 15's stem phase
+    unroll<0, 8>(block);
+    expand(IC<0>{});  // E's q = 1 copy was last read by block 7's stem phase (before its k-steps' barriers)
+    if constexpr (MODE == 2) {
+      int nfr, ny0, nx0;
+      tile_of(tl + 1, nfr, ny0, nx0);
+      load_window(nfr, ny0, nx0);  // the next tile's window, in registers until its store_window
+    }
+    auto blk2 = [&](auto bc) __attribute__((always_inline)) { block(IC<8 + decltype(bc)::value>{}); };
+    unroll<0, 8>(blk2);
     epilogue(cur_fr, cur_y0, cur_x0);
     tile_of(tl + 1, cur_fr, cur_y0, cur_x0);
-    lds_barrier();  // block 15's k-steps are done with N's and E's last readers
+    lds_barrier();  // block 15's k-steps are done with the halo / E before the next tile's writes
   }
 }
 

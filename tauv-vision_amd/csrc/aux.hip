@@ -210,17 +210,35 @@ int launch_leaky_inplace(float* x, size_t n, hipStream_t s) {
   return 0;
 }
 
-// one thread per (target pixel, 16-byte chunk); covered rectangle [y0,y1) x [x0,x1) skipped
+// the target pixels outside the ConvT's covered rectangle [y0,y1) x [x0,x1) take the skip tensor
+// as is (pad_to_match's zero margin + add). One thread per (uncovered pixel, 16-byte chunk): per
+// image the band above the rectangle (y0 rows), the band below it (tH - y1 rows) and the columns
+// left / right of it in its rows, enumerated in that order — the grid covers only those pixels
+// (the covered interior, nearly all of the target, launches nothing)
 __global__ void uncovered_copy(const uint4* __restrict__ add, int add_ldc16, uint4* __restrict__ out,
-                               int out_ldc16, int chunks, int B, int tH, int tW, int y0, int y1, int x0, int x1) {
-  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  size_t total = (size_t)B * tH * tW * chunks;
-  if (i >= total) return;
-  int c = i % chunks;
-  size_t pix = i / chunks;
-  int x = pix % tW;
-  int y = (pix / tW) % tH;
-  if (y >= y0 && y < y1 && x >= x0 && x < x1) return;
+                               int out_ldc16, int chunks, int B, int tH, int tW, int y0, int y1, int x0, int x1,
+                               int per_img) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * per_img * chunks) return;
+  const int c = (int)(i % chunks);
+  const long long q = i / chunks;
+  const int b = (int)(q / per_img);
+  int r = (int)(q - (long long)b * per_img);
+  const int ntop = y0 * tW, nbot = (tH - y1) * tW, side = x0 + (tW - x1);
+  int y, x;
+  if (r < ntop) {
+    y = r / tW;
+    x = r - y * tW;
+  } else if ((r -= ntop) < nbot) {
+    y = y1 + r / tW;
+    x = r - (y - y1) * tW;
+  } else {
+    r -= nbot;
+    const int k = r / side, m = r - k * side;
+    y = y0 + k;
+    x = m < x0 ? m : x1 + (m - x0);
+  }
+  const size_t pix = ((size_t)b * tH + y) * tW + x;
   out[pix * out_ldc16 + c] = add[pix * add_ldc16 + c];
 }
 
@@ -231,10 +249,16 @@ int launch_uncovered_copy(const void* add, int add_ldc, void* out, int out_ldc, 
     set_error("uncovered_copy: rows must be whole 16-byte chunks");
     return 1;
   }
-  int chunks = C * es / 16;
-  size_t total = (size_t)B * tH * tW * chunks;
-  hipLaunchKernelGGL(uncovered_copy, dim3((total + 255) / 256), dim3(256), 0, s, (const uint4*)add,
-                     add_ldc * es / 16, (uint4*)out, out_ldc * es / 16, chunks, B, tH, tW, y0, y1, x0, x1);
+  y0 = std::max(0, std::min(y0, tH));
+  y1 = std::max(y0, std::min(y1, tH));
+  x0 = std::max(0, std::min(x0, tW));
+  x1 = std::max(x0, std::min(x1, tW));
+  const int chunks = C * es / 16;
+  const int per_img = tH * tW - (y1 - y0) * (x1 - x0);
+  const long long total = (long long)B * per_img * chunks;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(uncovered_copy, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const uint4*)add,
+                     add_ldc * es / 16, (uint4*)out, out_ldc * es / 16, chunks, B, tH, tW, y0, y1, x0, x1, per_img);
   TV_HIP(hipGetLastError());
   return 0;
 }

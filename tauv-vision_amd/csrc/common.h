@@ -202,6 +202,7 @@ struct StemS2Params {
   int out_ldc;
   void* res;              // stem(2y, 2x), NHWC [B,Ho,Wo,res_ldc]
   int res_ldc;
+  unsigned long long* dbg;  // stamp builds (TV_C3_EXP=9) only: 8 cycle buckets per wave, else null
 };
 int stem_s2_tiles(int B, int Ho, int Wo);
 size_t stem_s2_weight_bytes();

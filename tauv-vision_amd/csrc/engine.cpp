@@ -988,6 +988,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     sp.out_ldc = t1.C;
     sp.res = base + ws->off[op.out2];
     sp.res_ldc = plan.tensors[op.out2].C;
+    if (stamp_op == (int)i) sp.dbg = stamp_buf;
     return launch_stem_s2(sp, dtype, cu_count, s);
   }
   if ((int)i == stem_op) {

@@ -43,8 +43,28 @@
 
 #include <type_traits>
 
+#ifndef TV_C3_EXP
+#define TV_C3_EXP 0  // 9: the stamp build (conv3x3_kernel.h) — per-wave cycle buckets into StemS2Params.dbg
+#endif
+#if TV_C3_EXP == 9
+#define SS2_STAMP(B)                                                                   \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    unsigned long long t_;                                                             \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    if (lane == 0) st_b[B] += (unsigned)t_ - st_last; /* LDS: no SGPRs held */         \
+    st_last = (unsigned)t_;                                                            \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#else
+#define SS2_STAMP(B) \
+  do {               \
+  } while (0)
+#endif
+
 #ifndef TV_SS2_EXP
-#define TV_SS2_EXP 0  // timing-only diagnostic builds (wrong results): 1 = no stem MFMAs
+#define TV_SS2_EXP 0  // timing-only diagnostic builds (wrong results): 1 = no stem MFMAs, 3 = k-step barriers only
+                      // at a block's first k-step, 4 = no conv1 weight staging (ring loads / writes)
 #endif
 
 namespace tv {
@@ -210,6 +230,18 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   const int ntl = first < end ? (end - first + stride - 1) / stride : 0;
   if (ntl == 0) return;
+#if TV_C3_EXP == 9
+  // buckets: 0 block barrier wait, 1 stem phase, 2 k-step barrier wait (+ a block's first reads),
+  // 3 k-step MFMA halves, 4 staging under the k-steps, 5 epilogue, 6 prologue / tile end, 7 k-steps
+  unsigned* st_b = reinterpret_cast<unsigned*>(smem + LDS) + wave * 8;  // the stamp build's extra LDS
+  if (lane < 8) st_b[lane] = 0;
+  unsigned st_last;
+  {
+    unsigned long long t0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+    st_last = (unsigned)t0;
+  }
+#endif
   auto tile_of = [&](int idx, int& fr, int& oy0, int& ox0) __attribute__((always_inline)) {
     const int t = first + min(idx, ntl - 1) * stride;  // past the list: the last tile again
     fr = t / tiles_f;
@@ -293,9 +325,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
   // N -> E for column parity Q: E[r][hx] = the 24 values from window pixel 2 hx - Q + 1 on
   // (7 horizontal taps x 3 channels of stem column 2 ox0 + 2 hx - Q; values 21..23 zero)
-  auto expand = [&](auto qc) __attribute__((always_inline)) {
+  // (part `part` of `nparts`: the entries idx = tid + NT (part + nparts n))
+  auto expand = [&](auto qc, int part, int nparts) __attribute__((always_inline)) {
     constexpr int Q = decltype(qc)::value, NC = TW + Q, TOT = WR * NC * 3;
-    for (int idx = opaque(tid); idx < TOT; idx += NT) {
+    for (int idx = opaque(tid) + part * NT; idx < TOT; idx += nparts * NT) {
       const int pp = idx % 3, e = idx / 3;
       const int r = e / NC, hx = e - r * NC;
       const int boff = r * NPITCH + 6 * (2 * hx - Q + 1) + 16 * pp;
@@ -437,7 +470,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   Half H0, H1;
-  int cur_fr = 0, cur_y0 = 0, cur_x0 = 0;
+  int cur_fr = 0, cur_y0 = 0, cur_x0 = 0, nx_fr = 0, nx_y0 = 0, nx_x0 = 0;
   // one conv1 k-step at schedule position QS of the tile (block SCH.blk, tap j)
   auto step = [&](auto qc) __attribute__((always_inline)) {
     constexpr int QS = decltype(qc)::value;
@@ -446,8 +479,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     constexpr int PAR = QS & 3, SLOT = QS % RING;
     constexpr bool FIRST = QS == 0;  // the tile's first products
     static_assert(SPT % 4 == 0 && SPT % RING == 0, "static register set / ring slot per position");
+    SS2_STAMP(3);  // (the previous k-step's tail, or the stem phase's when FIRSTK: charged below)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if TV_SS2_EXP == 3
+    if constexpr (FIRSTK) __builtin_amdgcn_s_barrier();
+#else
     __builtin_amdgcn_s_barrier();  // the block's halo (stem phase) / k-step QS + 1's weights visible
+#endif
     __builtin_amdgcn_sched_barrier(0);
     const unsigned wc0 = wa[0] + (unsigned)(SLOT * WSLOT);
     const unsigned wc1 = wa[1] + (unsigned)(SLOT * WSLOT);
@@ -458,6 +496,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
+    SS2_STAMP(2);
+#if TV_C3_EXP == 9
+    if (lane == 0) st_b[7] += 1;
+#endif
     // first half: sub-step 0 (H0) MFMAs, channel fragment by channel fragment, with sub-step 1's
     // reads (H1) and the ring write issued between them
     mfma_col(IC<0>{}, IC<FIRST>{}, H0);
@@ -468,7 +510,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     read_one(IC<2>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
     read_one(IC<3>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
     // k-step QS + 2 (loaded at step QS - 3) into the slot k-step QS - 1 used (read before this barrier)
+#if TV_SS2_EXP != 4
     w_store((QS + 2) % RING, wreg[(PAR + 2) & 3]);
+#endif
     __builtin_amdgcn_sched_barrier(0);
     mfma_col(IC<2>{}, IC<FIRST>{}, H0);
     read_one(IC<4>{}, IC<1>{}, IC<J>{}, xa, wc1, H1);
@@ -481,7 +525,9 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     __builtin_amdgcn_sched_barrier(0);
     // second half: sub-step 1 (H1), the next k-step's sub-step-0 reads (within the block) between
     mfma_col(IC<0>{}, IC<false>{}, H1);
+#if TV_SS2_EXP != 4
     w_load(wreg[(PAR + 1) & 3]);  // k-step QS + 5 (past the tile's end: the next tile's, same weights)
+#endif
     if constexpr (!LASTK) {
       read_one(IC<0>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
       read_one(IC<1>{}, IC<0>{}, IC<J + 1>{}, xa, wn0, H0);
@@ -501,6 +547,20 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     __builtin_amdgcn_sched_barrier(0);
     mfma_col(IC<3>{}, IC<false>{}, H1);
     __builtin_amdgcn_sched_barrier(0);
+    SS2_STAMP(3);
+    // u8 frames (the product path): the tile's serial staging moved under the k-steps, where the
+    // SIMD's other wave keeps issuing MFMAs — E for q = 0 under block 7 (E's q = 1 copy was last
+    // read by block 7's stem phase, before these k-steps' barriers), the next tile's window into
+    // registers at block 8, into N at block 12 (N was last read by the expansion under block 7),
+    // the next tile's E for q = 1 under block 15 (E's q = 0 copy was last read by block 15's stem)
+    if constexpr (MODE == 2) {
+      if constexpr (BLK == 7) expand(IC<0>{}, TB, L);
+      if constexpr (BLK == 8 && TB == 0) load_window(nx_fr, nx_y0, nx_x0);
+      if constexpr (BLK == 12 && TB == 0) store_window(nx_y0, nx_x0);
+      if constexpr (BLK == 15) expand(IC<1>{}, TB, L);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    SS2_STAMP(4);
   };
 
   // conv1 epilogue: bias + activation + 16-byte stores (out-of-range pixels: dropped)
@@ -539,7 +599,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 
   // ---- prologue: tile 0's window, channel block 0's stem weights, conv1 weights of k-steps 0..4
   tile_of(0, cur_fr, cur_y0, cur_x0);
-  if constexpr (MODE == 2) load_window(cur_fr, cur_y0, cur_x0);
+  if constexpr (MODE == 2) load_window(cur_fr, cur_y0, cur_x0);  // (stored after the barrier below)
   load_stem_w(0);
   w_load(wreg[0]);
   w_load(wreg[1]);
@@ -553,33 +613,51 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // one block: [barrier] stem phase [stem weights of the next channel block] k-steps
   auto block = [&](auto bc) __attribute__((always_inline)) {
     constexpr int B = decltype(bc)::value;
+    SS2_STAMP(6);
     lds_barrier();  // the previous block's k-steps have read the halo
+    SS2_STAMP(0);
     stem_phase(IC<B>{}, cur_y0, cur_x0);
     if constexpr (blk_p(B) == 1) load_stem_w(blk_cb((B + 1) % NBLK));  // lands under this block's k-steps
+    SS2_STAMP(1);
     auto ks = [&](auto t) __attribute__((always_inline)) {
       constexpr int T_ = decltype(t)::value;
       step(IC<SCH.first[B] + T_>{});
     };
     unroll<0, pb_len(blk_p(B), blk_q(B))>(ks);
   };
-  for (int tl = 0; tl < ntl; ++tl) {
-    if constexpr (MODE != 2) load_window(cur_fr, cur_y0, cur_x0);
-    store_window(cur_y0, cur_x0);  // N was last read by expand<0> in the previous tile
+  if constexpr (MODE == 2) {  // the first tile's N and E (later tiles': under the previous tile)
+    store_window(cur_y0, cur_x0);
     lds_barrier();
-    expand(IC<1>{});               // E was last read by block 15's stem phase
-    unroll<0, 8>(block);
-    expand(IC<0>{});  // E's q = 1 copy was last read by block 7's stem phase (before its k-steps' barriers)
-    if constexpr (MODE == 2) {
-      int nfr, ny0, nx0;
-      tile_of(tl + 1, nfr, ny0, nx0);
-      load_window(nfr, ny0, nx0);  // the next tile's window, in registers until its store_window
+    expand(IC<1>{}, 0, 1);
+  }
+  for (int tl = 0; tl < ntl; ++tl) {
+    tile_of(tl + 1, nx_fr, nx_y0, nx_x0);  // (past the list: this tile again)
+    if constexpr (MODE != 2) {
+      load_window(cur_fr, cur_y0, cur_x0);
+      store_window(cur_y0, cur_x0);  // N was last read by expand<0> in the previous tile
+      lds_barrier();
+      expand(IC<1>{}, 0, 1);         // E was last read by block 15's stem phase
     }
+    unroll<0, 8>(block);
+    if constexpr (MODE != 2) expand(IC<0>{}, 0, 1);  // E's q = 1 copy was last read by block 7's stem phase
     auto blk2 = [&](auto bc) __attribute__((always_inline)) { block(IC<8 + decltype(bc)::value>{}); };
     unroll<0, 8>(blk2);
+    SS2_STAMP(6);
     epilogue(cur_fr, cur_y0, cur_x0);
-    tile_of(tl + 1, cur_fr, cur_y0, cur_x0);
+    SS2_STAMP(5);
+    cur_fr = nx_fr;
+    cur_y0 = nx_y0;
+    cur_x0 = nx_x0;
     lds_barrier();  // block 15's k-steps are done with the halo / E before the next tile's writes
   }
+#if TV_C3_EXP == 9
+  SS2_STAMP(6);
+  if (p.dbg && lane == 0) {
+    unsigned long long* d = p.dbg + ((size_t)blockIdx.x * NWV + wave) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = st_b[k];  // (< 2^32 cycles per wave and bucket)
+  }
+#endif
 }
 
 // [Npad][Kpad] conv1 weights (K = tap * 128 + channel) -> [k-step s][128 rows][4 x 16 B] in this
@@ -597,8 +675,9 @@ __global__ void repack_weights(const uint4* __restrict__ w, int kpad16, uint4* _
 template <typename T, int MODE>
 static int launch_t(const StemS2Params& p, int grid, hipStream_t s) {
   auto k = stem_s2<T, MODE>;
-  if (int r = ensure_lds<stem_s2<T, MODE>>(LDS)) return r;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), LDS, s, p);
+  constexpr int lds = LDS + (TV_C3_EXP == 9 ? NWV * 8 * 4 : 0);  // (the stamp build's buckets)
+  if (int r = ensure_lds<stem_s2<T, MODE>>(lds)) return r;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, p);
   TV_HIP(hipGetLastError());
   return 0;
 }

@@ -411,23 +411,18 @@ def cpu_baseline(sd, seconds, K, thr, arch="r18"):
 YOLACT_METRIC = "frames/sec YOLACT protonet + box decode + fast NMS + mask assembly 550x550 batch=32 + %roofline"
 
 
-def run_yolact(args, world, rank, device):
-    """BASELINE config 5 (YOLACT 550x550, batch 32): one step = fpn[0] [B, 256, 69, 69] resident
-    in HBM -> Masknet protonet (masknet.py:8-55; F = 256, k = 8 prototypes, train.py:28-33) ->
-    box_decode of every anchor (boxes.py:55-61; 6416 anchors at 550x550) -> fast NMS per image
-    (nms.py:7-29; top_k 100 as evaluate_batch.py:51, IoU 0.5, confidence 0.05) -> assemble_mask
-    of the kept detections (masks.py:8-21, at prototype resolution 276x276) -> counts to host.
-    The ResNet backbone / FPN / prediction head are not on the north-star path (they need
-    torchvision, absent here): their outputs are synthetic tensors of the reference's shapes."""
+def yolact_setup(B, precision, device, rank=0):
+    """The YOLACT step's resident inputs and its step function (run_yolact; tools/prof_forward.py
+    --model yolact for the PMC passes). Synthetic fpn[0] / head outputs of the reference shapes."""
     from tauv_vision_amd.yolact import (Masknet, YolactConfig, BatchedNMS, box_decode, get_anchor,
                                         assemble_masks_indexed)
-    B, F, k, C1 = args.batch if args.batch != 64 else 32, 256, 8, 8
+    F, k, C1 = 256, 8, 8
     cfg = YolactConfig(550, 550, (24, 48, 96, 192, 384), (1,), (0.1, 0.2), feature_depth=F, n_prototype_masks=k)
     fpn = [(69, 69), (35, 35), (18, 18), (9, 9), (5, 5)]
     anchor = torch.cat([get_anchor(i, s, cfg) for i, s in enumerate(fpn)], 1).to(device)
     A = anchor.shape[1]
     top_k = 100
-    net = Masknet(cfg, precision=args.precision)
+    net = Masknet(cfg, precision=precision)
     g = torch.Generator(device=device).manual_seed(2000 + rank)
     x = torch.randn((B, F, 69, 69), generator=g, device=device)
     cls = torch.randn((B, A, C1), generator=g, device=device) * 2.0
@@ -448,6 +443,25 @@ def run_yolact(args, world, rank, device):
         det, cnt = bnms(cls, box, 0.5, 0.05)
         assemble_masks_indexed(pview, coeff, box, det, cnt, out=masks)
         host_counts.copy_(cnt, non_blocking=True)
+
+    return dict(cfg=cfg, anchor=anchor, A=A, top_k=top_k, net=net, x=x, cls=cls, enc=enc, coeff=coeff, eng=eng,
+                proto=proto, pview=pview, bnms=bnms, masks=masks, box_out=box_out, step=step, k=k, F=F)
+
+
+def run_yolact(args, world, rank, device):
+    """BASELINE config 5 (YOLACT 550x550, batch 32): one step = fpn[0] [B, 256, 69, 69] resident
+    in HBM -> Masknet protonet (masknet.py:8-55; F = 256, k = 8 prototypes, train.py:28-33) ->
+    box_decode of every anchor (boxes.py:55-61; 6416 anchors at 550x550) -> fast NMS per image
+    (nms.py:7-29; top_k 100 as evaluate_batch.py:51, IoU 0.5, confidence 0.05) -> assemble_mask
+    of the kept detections (masks.py:8-21, at prototype resolution 276x276) -> counts to host.
+    The ResNet backbone / FPN / prediction head are not on the north-star path (they need
+    torchvision, absent here): their outputs are synthetic tensors of the reference's shapes."""
+    from tauv_vision_amd.yolact import box_decode, assemble_masks_indexed
+    B = args.batch if args.batch != 64 else 32
+    w = yolact_setup(B, args.precision, device, rank)
+    cfg, anchor, A, top_k, net, k, F = w["cfg"], w["anchor"], w["A"], w["top_k"], w["net"], w["k"], w["F"]
+    x, cls, enc, coeff, proto, pview = w["x"], w["cls"], w["enc"], w["coeff"], w["proto"], w["pview"]
+    eng, bnms, masks, box_out, step = w["eng"], w["bnms"], w["masks"], w["box_out"], w["step"]
 
     elapsed = timed(step, args.steps, args.warmup, world, device)
     value = world * B * args.steps / elapsed
@@ -470,7 +484,8 @@ def run_yolact(args, world, rank, device):
     name, (n, ms, fl) = max(kern.items(), key=lambda kv: kv[1][1])
     peak = PEAK_TFLOPS[args.precision]
     roof = {"bound": "mfma", "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4), "traffic": None, "launch_batch": B,
+            "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4),
+            "traffic": load_traffic(name, B, args.precision, "yolact"), "launch_batch": B,
             "kernel": f"{name}: {n} launches/forward, avg {ms / n:.4f} ms, avg {fl / n / 1e9:.2f} GFLOP/launch",
             "per_kernel": {kn: {"launches": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / v[1] / 1e9, 1)}
                            for kn, v in kern.items()},

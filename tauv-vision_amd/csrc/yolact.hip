@@ -380,6 +380,89 @@ __global__ __launch_bounds__(kMaskThreads) void assemble_mask(const MaskParams p
   }
 }
 
+// assemble_mask for K <= KT prototypes: the same arithmetic with each thread's 4 pixels x K
+// prototype values held in registers (loaded once) instead of re-read from LDS for every
+// detection — the LDS variant above read 8 x 16 B of prototypes per 16 B written and ran at
+// ~3 TB/s; here a detection costs two broadcast LDS reads per thread (its coefficients and
+// bounds), and the kernel runs at the write stream
+template <int KT>
+__global__ __launch_bounds__(kMaskThreads) void assemble_mask_reg(const MaskParams p) {
+  __shared__ float dc[kMaskDets * KT];  // [kMaskDets][KT] coefficients (zero past K)
+  __shared__ float4 db4[kMaskDets];     // left, right, top, bottom
+  const int b = blockIdx.y;
+  const int n = p.counts ? min(p.counts[b], p.n_max) : p.n_max;
+  if (n <= 0) return;
+  const int hw = p.H * p.W;
+  const int pix = blockIdx.x * kMaskPix + 4 * threadIdx.x;
+  const float* pb = p.proto + (size_t)b * p.ps_b;
+  int yy[4], xx[4];
+  float pv[KT][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int q = min(pix + e, hw - 1);
+    yy[e] = q / p.W;
+    xx[e] = q - yy[e] * p.W;
+  }
+#pragma unroll
+  for (int k = 0; k < KT; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      pv[k][e] = k < p.K ? pb[(size_t)k * p.ps_k + (size_t)yy[e] * p.ps_y + (size_t)xx[e] * p.ps_x] : 0.f;
+  const bool vec = (hw & 3) == 0;
+  const float* cb = p.coeff + (size_t)b * p.rows * p.K;
+  const float* bb = p.box ? p.box + (size_t)b * p.rows * 4 : nullptr;
+  const long long* db = p.det ? p.det + (size_t)b * p.n_max : nullptr;
+  float* ob = p.out + (size_t)b * p.n_max * hw;
+  for (int d0 = 0; d0 < n; d0 += kMaskDets) {
+    const int nd = min(kMaskDets, n - d0);
+    __syncthreads();  // the previous chunk consumed
+    for (int e = threadIdx.x; e < nd * KT; e += kMaskThreads) {
+      const int d = e / KT, k = e - d * KT;
+      const size_t row = db ? (size_t)db[d0 + d] : (size_t)(d0 + d);
+      dc[e] = k < p.K ? cb[row * p.K + k] : 0.f;
+    }
+    if (bb)
+      for (int d = threadIdx.x; d < nd; d += kMaskThreads) {
+        const size_t row = db ? (size_t)db[d0 + d] : (size_t)(d0 + d);
+        const float* q = bb + row * 4;
+        const float by = q[0] * (float)p.H, bx = q[1] * (float)p.W, bh = q[2] * (float)p.H, bw = q[3] * (float)p.W;
+        db4[d] = make_float4(bx - bw / 2, bx + bw / 2, by - bh / 2, by + bh / 2);
+      }
+    __syncthreads();
+    if (pix >= hw) continue;
+    for (int d = 0; d < nd; ++d) {
+      const float* c = dc + d * KT;
+      float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {  // (k >= K: zero products; s is never -0, so adding them is exact)
+        const float ck = c[k];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[e] += ck * pv[k][e];
+      }
+      float m[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        m[e] = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-s[e] * 1.4426950408889634f));
+      if (bb) {
+        const float4 bd = db4[d];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float fx = (float)xx[e], fy = (float)yy[e];
+          m[e] *= (fx >= bd.x && fx <= bd.y && fy >= bd.z && fy <= bd.w) ? 1.f : 0.f;
+        }
+      }
+      float* o = ob + (size_t)(d0 + d) * hw + pix;
+      if (vec) {
+        *reinterpret_cast<float4*>(o) = make_float4(m[0], m[1], m[2], m[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (pix + e < hw) o[e] = m[e];
+      }
+    }
+  }
+}
+
 }  // namespace yolact
 
 int launch_yolact_box_decode(const float* enc, const float* anchor, int B, int A, int anchor_batch, float v0, float v1,
@@ -501,6 +584,16 @@ int launch_yolact_assemble_mask(const float* proto, const long long pst[4], int 
     return 2;  // TV_ESHAPE
   }
   if (n_max == 0) return 0;
+  yolact::MaskParams p{proto, pst[0], pst[1], pst[2], pst[3], K, H, W, coeff, box, counts, det, det ? rows : n_max,
+                       n_max, out};
+  const int hw = H * W;
+  const dim3 grid((hw + yolact::kMaskPix - 1) / yolact::kMaskPix, B);
+  if (K <= 16) {  // prototypes in registers (the protonet's k = 8; any K up to 16)
+    if (K <= 8) hipLaunchKernelGGL(yolact::assemble_mask_reg<8>, grid, dim3(yolact::kMaskThreads), 0, s, p);
+    else hipLaunchKernelGGL(yolact::assemble_mask_reg<16>, grid, dim3(yolact::kMaskThreads), 0, s, p);
+    TV_HIP(hipGetLastError());
+    return 0;
+  }
   const size_t lds = ((size_t)K * yolact::kMaskPix + (size_t)yolact::kMaskDets * (K + 4)) * sizeof(float);
   if (lds > 160 * 1024) { set_error("assemble_mask: more than 37 prototypes"); return 2; }
   static std::once_flag attr_once;
@@ -510,11 +603,7 @@ int launch_yolact_assemble_mask(const float* proto, const long long pst[4], int 
                                    160 * 1024);
   });
   TV_HIP(attr_err);
-  yolact::MaskParams p{proto, pst[0], pst[1], pst[2], pst[3], K, H, W, coeff, box, counts, det, det ? rows : n_max,
-                       n_max, out};
-  const int hw = H * W;
-  hipLaunchKernelGGL(yolact::assemble_mask, dim3((hw + yolact::kMaskPix - 1) / yolact::kMaskPix, B),
-                     dim3(yolact::kMaskThreads), lds, s, p);
+  hipLaunchKernelGGL(yolact::assemble_mask, grid, dim3(yolact::kMaskThreads), lds, s, p);
   TV_HIP(hipGetLastError());
   return 0;
 }

@@ -218,6 +218,26 @@ def test_gpu_assemble_masks_batched():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K", [3, 8, 12, 16, 20, 37])
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
+def test_gpu_assemble_mask_prototype_counts(K, layout):
+    """Both mask kernels (prototypes in registers for K <= 16 in two widths, LDS-staged above),
+    NCHW and NHWC prototype storage, a width not a multiple of 4 (scalar stores) and one that is."""
+    from tauv_vision_amd.yolact import assemble_mask
+    g = torch.Generator().manual_seed(K)
+    for H, W in ((19, 23), (16, 36)):
+        p = torch.randn(K, H, W, generator=g)
+        proto = p.cuda() if layout == "nchw" else p.permute(1, 2, 0).contiguous().cuda().permute(2, 0, 1)
+        n = 70  # two detection chunks of the kernels
+        coeff = torch.randn(n, K, generator=g)
+        box = torch.cat([torch.rand(n, 2, generator=g), torch.rand(n, 2, generator=g) * 0.6], -1)
+        for bx in (box, None):
+            got = assemble_mask(proto, coeff.cuda(), None if bx is None else bx.cuda()).cpu().numpy()
+            ref = ry.assemble_mask(p, coeff, bx).numpy()
+            np.testing.assert_allclose(got, ref, rtol=0, atol=1e-6)
+
+
+@pytest.mark.gpu
 def test_gpu_assemble_masks_rejects_bad_out():
     """A caller-supplied `out` / index tensor reaches the kernel as a raw pointer: wrong shape,
     dtype, layout or device is refused before any launch (nothing is written)."""

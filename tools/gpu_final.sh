@@ -26,11 +26,12 @@ done
 step prof_r18 300 rocprofv3 --kernel-trace --stats -d $O/prof -o r18 --output-format csv -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-b1 --no-extras
 step prof_dla34 300 rocprofv3 --kernel-trace --stats -d $O/prof -o dla34 --output-format csv -- python bench.py --model dla34 --steps 10 --warmup 3 --no-cpu-baseline --no-b1 --no-extras
 step prof_yolact 300 rocprofv3 --kernel-trace --stats -d $O/prof -o yolact --output-format csv -- python bench.py --model yolact --steps 5 --warmup 2 --no-cpu-baseline --no-extras
-for m in r18 dla34; do
+for m in r18 dla34 yolact; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $c -d $O/pmc/$m -o $c --output-format csv -- python tools/prof_forward.py --iters 1 --model $m > $O/pmc/${m}_$c.log 2>&1
     echo "pmc $m $c rc=$?"
   done
+  [ $m = yolact ] && continue
   timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES -d $O/pmc/$m -o mfma --output-format csv -- python tools/prof_forward.py --iters 1 --model $m > $O/pmc/${m}_mfma.log 2>&1
   echo "pmc $m mfma rc=$?"
 done

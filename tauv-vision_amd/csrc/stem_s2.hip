@@ -62,6 +62,10 @@
   } while (0)
 #endif
 
+#ifndef SS2_RD_AHEAD
+#define SS2_RD_AHEAD 2  // stem-phase operands (E reads) in flight per wave
+#endif
+
 #ifndef TV_SS2_EXP
 #define TV_SS2_EXP 0  // timing-only diagnostic builds (wrong results): 1 = no stem MFMAs, 3 = k-step barriers only
                       // at a block's first k-step, 4 = no conv1 weight staging (ring loads / writes)
@@ -326,27 +330,36 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // N -> E for column parity Q: E[r][hx] = the 24 values from window pixel 2 hx - Q + 1 on
   // (7 horizontal taps x 3 channels of stem column 2 ox0 + 2 hx - Q; values 21..23 zero)
   // (part `part` of `nparts`: the entries idx = tid + NT (part + nparts n))
+  // Thread t < 5 x 3 NC owns one (pixel hx, part pp) column of E and rows r0 + 5 i (r0 = t / 3 NC):
+  // one division per call, and compile-time LDS offsets from two base addresses per row step.
   auto expand = [&](auto qc, int part, int nparts) __attribute__((always_inline)) {
-    constexpr int Q = decltype(qc)::value, NC = TW + Q, TOT = WR * NC * 3;
-    for (int idx = opaque(tid) + part * NT; idx < TOT; idx += nparts * NT) {
-      const int pp = idx % 3, e = idx / 3;
-      const int r = e / NC, hx = e - r * NC;
-      const int boff = r * NPITCH + 6 * (2 * hx - Q + 1) + 16 * pp;
-      const unsigned* d = reinterpret_cast<const unsigned*>(smem + OFF_N + (boff & ~3));
-      const unsigned sh = (unsigned)(boff & 3);  // 0 or 2
-      unsigned v[5];
+    constexpr int Q = decltype(qc)::value, NC = TW + Q, NU = 3 * NC, RSTEP = NT / NU;
+    constexpr int NI = (WR + RSTEP - 1) / RSTEP;
+    static_assert(RSTEP == 5 && NI == 8, "5 rows per pass, 8 passes");
+    const int t = opaque(tid);
+    const int r0 = t / NU, u = t - r0 * NU;
+    const int hx = u / 3, pp = u - hx * 3;
+    const int boff = r0 * NPITCH + 6 * (2 * hx - Q + 1) + 16 * pp;
+    const char* src = smem + OFF_N + (boff & ~3);
+    char* dst = smem + OFF_E + (r0 * ECOLS + hx) * EPIX + 16 * pp;
+    const unsigned sh = (unsigned)(boff & 3);  // 0 or 2
+    const unsigned mz = pp == 2 ? 0xffffu : 0xffffffffu, mw = pp == 2 ? 0u : 0xffffffffu;
+    if (r0 < RSTEP) {
 #pragma unroll
-      for (int j = 0; j < 5; ++j) v[j] = d[j];
-      uint4 o;
-      o.x = __builtin_amdgcn_alignbyte(v[1], v[0], sh);
-      o.y = __builtin_amdgcn_alignbyte(v[2], v[1], sh);
-      o.z = __builtin_amdgcn_alignbyte(v[3], v[2], sh);
-      o.w = __builtin_amdgcn_alignbyte(v[4], v[3], sh);
-      if (pp == 2) {
-        o.z &= 0xffffu;
-        o.w = 0u;
+      for (int i = 0; i < NI; ++i) {
+        if (i < part * NI / nparts || i >= (part + 1) * NI / nparts) continue;
+        if (r0 + RSTEP * i >= WR) continue;
+        const unsigned* d = reinterpret_cast<const unsigned*>(src + i * RSTEP * NPITCH);
+        unsigned v[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) v[j] = d[j];
+        uint4 o;
+        o.x = __builtin_amdgcn_alignbyte(v[1], v[0], sh);
+        o.y = __builtin_amdgcn_alignbyte(v[2], v[1], sh);
+        o.z = __builtin_amdgcn_alignbyte(v[3], v[2], sh) & mz;
+        o.w = __builtin_amdgcn_alignbyte(v[4], v[3], sh) & mw;
+        *reinterpret_cast<uint4*>(dst + i * RSTEP * ECOLS * EPIX) = o;
       }
-      *reinterpret_cast<uint4*>(smem + OFF_E + (r * ECOLS + hx) * EPIX + 16 * pp) = o;
     }
   };
 
@@ -361,8 +374,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 
   // ---- stem phase: the halo of phase block (P, Q), channel block CB of tile (oy0, ox0) into LDS.
   // Fragment k = 32 consecutive pixels of the (16 + P) x (32 + Q) block (row-major); wave w
-  // computes fragments w, w + 4, ... two at a time (independent accumulators keep the one wave
-  // of the SIMD issuing back to back); lane (l32, lh): pixel l32, K half lh.
+  // computes fragments w, w + 8, ... (a single accumulation chain issues back to back,
+  // MI355X_MICROARCH.md); lane (l32, lh): pixel l32, K half lh.
   auto stem_phase = [&](auto bc, int oy0, int ox0) __attribute__((always_inline)) {
     constexpr int B = decltype(bc)::value;
     constexpr int P = blk_p(B), Q = blk_q(B), CB = blk_cb(B);
@@ -376,18 +389,30 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       const char* e0 = smem + OFF_E + ((2 * hy - P + 1) * ECOLS + hx) * EPIX;
       const char* e16 = e0 + lh * 16;
       const char* erow = e0 + lh * (ECOLS * EPIX - 32);
-      f32x16 acc = f32x16{};
-#pragma unroll
-      for (int j = 0; j < KS; ++j) {
+      auto rd = [&](int j) __attribute__((always_inline)) {
         const int c0 = 2 * j;  // lane half 0's chunk (ky = c0 / 3, part = c0 % 3); half 1 reads c0 + 1
         const int off = (c0 / 3) * ECOLS * EPIX + (c0 % 3) * 16;
         const char* base = j == KS - 1 ? e0 : (c0 % 3 == 2 ? erow : e16);  // (k-step 10's half 1: zero weights)
-        const uint4 b = *reinterpret_cast<const uint4*>(base + off);
+        return *reinterpret_cast<const uint4*>(base + off);
+      };
+      // operands RA k-steps ahead through a register ring: left to itself the compiler re-used
+      // one register set, one LDS round trip exposed before every MFMA (1.33 -> 1.25-1.27 ms per
+      // slice with 2 or 4 ahead; the next fragment's first operands issued before this one's
+      // epilogue as well: no further change, profiles/r4l, r4m)
+      constexpr int RA = SS2_RD_AHEAD;
+      uint4 bq[RA];
+#pragma unroll
+      for (int j = 0; j < RA; ++j) bq[j] = rd(j);
+      f32x16 acc = f32x16{};
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
 #if TV_SS2_EXP == 1
-        acc[j] += __uint_as_float(b.x ^ wst[j].y);
+        acc[j] += __uint_as_float(bq[j % RA].x ^ wst[j].y);
 #else
-        Mfma<T>::run(wst[j], b, acc);
+        Mfma<T>::run(wst[j], bq[j % RA], acc);
 #endif
+        if (j + RA < KS) bq[j % RA] = rd(j + RA);
+        __builtin_amdgcn_sched_barrier(0);
       }
       const int sy = 2 * oy0 + 2 * hy - P, sx = 2 * ox0 + 2 * hx - Q;
       const bool in = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;

@@ -14,7 +14,10 @@
 //               = the reference's stable descending sort, equal confidences in ascending anchor
 //               order) in registers, the K-th largest found by 8 radix passes of 8-bit digits
 //               over LDS histograms, the K keys >= it compacted into LDS and bitonic-sorted;
-//               larger top_k / anchor counts take a rocPRIM segmented radix sort (the same order);
+//   nms_sort    larger top_k / anchor counts (up to the full sort): one workgroup per image
+//               streams the keys from L2 instead of holding them, and sorts the top K in rank
+//               ranges of <= 16384 keys (each range's lower bound = one more radix select,
+//               its keys compacted into LDS and bitonic-sorted): the same order, no library;
 //   nms_iou     one thread per kept column j < min(top_k, A); rows i < j staged through LDS in
 //               256-box chunks; the column max propagates NaN like torch.max (0/0 IoUs of two
 //               zero-area boxes drop the column: NaN <= thr is false);
@@ -28,8 +31,6 @@
 
 #include <cstring>
 #include <mutex>
-#include <rocprim/device/device_segmented_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 // the reference rounds every product before the sum (separate torch ops): no FMA contraction
 #pragma clang fp contract(off)
@@ -262,9 +263,99 @@ __global__ __launch_bounds__(kTopkThreads) void nms_topk(const uint32_t* __restr
   }
 }
 
-__global__ void segment_offsets(int* off, int B, int A) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i <= B) off[i] = i * A;
+// ---- any top_k / anchor count (nms_sort) -----------------------------------------------------
+constexpr int kSortThreads = 1024;
+constexpr int kSortCap = 16384;  // keys per rank range (128 KiB of LDS)
+
+// 64-bit key of anchor a (the nms_topk order); never 0
+__device__ __forceinline__ unsigned long long nms_key(const uint32_t* __restrict__ keys, size_t seg, int a) {
+  return ((unsigned long long)keys[seg + a] << 32) | (0xFFFFFFFFu - (unsigned)a);
+}
+
+__global__ __launch_bounds__(kSortThreads) void nms_sort(const uint32_t* __restrict__ keys, int A, int K,
+                                                         uint32_t* __restrict__ skeys, int* __restrict__ sidx) {
+  extern __shared__ unsigned long long sel[];  // [kSortCap]
+  __shared__ unsigned hist[256];
+  __shared__ unsigned s_digit, s_above, s_n;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t seg = (size_t)b * A;
+  // the rank-th largest key (1 <= rank <= A): exactly `rank` keys are >= it (keys are unique)
+  auto select = [&](unsigned rank) {
+    unsigned long long prefix = 0, pmask = 0;
+    unsigned need = rank;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      if (tid < 256) hist[tid] = 0;
+      __syncthreads();
+      for (int a = tid; a < A; a += kSortThreads) {
+        const unsigned long long k = nms_key(keys, seg, a);
+        if ((k & pmask) == prefix) atomicAdd(&hist[(unsigned)(k >> shift) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid < 64) {  // one wave: the digit whose suffix count first reaches `need` (nms_topk)
+        const unsigned h0 = hist[255 - 4 * tid], h1 = hist[254 - 4 * tid], h2 = hist[253 - 4 * tid],
+                       h3 = hist[252 - 4 * tid];
+        const unsigned own = h0 + h1 + h2 + h3;
+        unsigned incl = own;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const unsigned o = __shfl_up(incl, d, 64);
+          if (tid >= d) incl += o;
+        }
+        const unsigned excl = incl - own;
+        if (excl < need && incl >= need) {
+          unsigned above = excl;
+          const unsigned hs[4] = {h0, h1, h2, h3};
+          int q = 0;
+          while (above + hs[q] < need) above += hs[q++];
+          s_digit = 255u - 4u * (unsigned)tid - (unsigned)q;
+          s_above = above;
+        }
+      }
+      __syncthreads();
+      prefix |= (unsigned long long)s_digit << shift;
+      pmask |= 255ull << shift;
+      need -= s_above;
+      __syncthreads();
+    }
+    return prefix;
+  };
+  unsigned long long hi = 0;  // the previous range's lower bound (exclusive upper bound of this one)
+  for (int r0 = 0; r0 < K; r0 += kSortCap) {
+    const int r1 = min(K, r0 + kSortCap), n = r1 - r0;
+    const unsigned long long lo = select((unsigned)r1);
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    for (int a = tid; a < A; a += kSortThreads) {
+      const unsigned long long k = nms_key(keys, seg, a);
+      if (k >= lo && (r0 == 0 || k < hi)) sel[atomicAdd(&s_n, 1u)] = k;  // exactly n keys
+    }
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int i = n + tid; i < n2; i += kSortThreads) sel[i] = 0;  // (0: below every key)
+    __syncthreads();
+    for (int size = 2; size <= n2; size <<= 1)  // bitonic sort, descending
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < n2; i += kSortThreads) {
+          const int j = i ^ stride;
+          if (j > i) {
+            const bool desc = (i & size) == 0;
+            const unsigned long long x = sel[i], y = sel[j];
+            if (desc ? x < y : x > y) {
+              sel[i] = y;
+              sel[j] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (int r = tid; r < n; r += kSortThreads) {
+      const unsigned long long key = sel[r];
+      skeys[seg + r0 + r] = (uint32_t)(key >> 32);
+      sidx[seg + r0 + r] = (int)(seg + (0xFFFFFFFFu - (uint32_t)key));
+    }
+    hi = lo;
+    __syncthreads();  // sel consumed before the next range's compaction
+  }
 }
 
 // masks[b][d][y][x] = sigmoid(sum_k coeff[b][d][k] * proto[b][k][y][x]) * box_mask(b, d, y, x)
@@ -494,29 +585,18 @@ int launch_yolact_box_encode(const float* box, const float* anchor, int B, int A
 namespace {
 
 struct NmsLayout {
-  size_t keys, skeys, sidx, keep, offs, tmp, tmp_bytes, total;
+  size_t keys, skeys, sidx, keep, total;
 };
 
 size_t al(size_t x) { return (x + 255) / 256 * 256; }
 
 int nms_layout(int B, int A, int K, NmsLayout* L) {
   const size_t n = (size_t)B * A;
-  size_t tmp_bytes = 0;
-  hipError_t e = rocprim::segmented_radix_sort_pairs_desc(
-      nullptr, tmp_bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr, rocprim::counting_iterator<int>(0),
-      (int*)nullptr, (unsigned)n, (unsigned)B, (const int*)nullptr, (const int*)nullptr, 0, 32, (hipStream_t)0);
-  if (e != hipSuccess) {
-    set_error(std::string("fast_nms: sort workspace query: ") + hipGetErrorString(e));
-    return 3;
-  }
   size_t o = 0;
   L->keys = o;  o += al(n * 4);
   L->skeys = o; o += al(n * 4);
   L->sidx = o;  o += al(n * 4);
   L->keep = o;  o += al((size_t)B * K);
-  L->offs = o;  o += al((size_t)(B + 1) * 4);
-  L->tmp = o;   o += al(tmp_bytes);
-  L->tmp_bytes = tmp_bytes;
   L->total = o;
   return 0;
 }
@@ -547,11 +627,8 @@ int launch_yolact_fast_nms(const float* cls, long long cls_bstride, int A, int C
   uint32_t* skeys = (uint32_t*)(w + L.skeys);
   int* sidx = (int*)(w + L.sidx);
   uint8_t* keep = (uint8_t*)(w + L.keep);
-  int* offs = (int*)(w + L.offs);
   const unsigned n = (unsigned)B * A;
   hipLaunchKernelGGL(yolact::nms_keys, dim3((n + 255) / 256), dim3(256), 0, s, cls, cls_bstride, A, C1, B, keys);
-  TV_HIP(hipGetLastError());
-  hipLaunchKernelGGL(yolact::segment_offsets, dim3((B + 256) / 256), dim3(256), 0, s, offs, B, A);
   TV_HIP(hipGetLastError());
   if (K <= yolact::kTopkMaxK && A <= 32 * yolact::kTopkThreads) {
     // (first K entries of each segment: all nms_iou / nms_compact read)
@@ -563,9 +640,15 @@ int launch_yolact_fast_nms(const float* cls, long long cls_bstride, int A, int C
       hipLaunchKernelGGL(yolact::nms_topk<32>, dim3(B), dim3(yolact::kTopkThreads), 0, s, keys, A, K, skeys, sidx);
     TV_HIP(hipGetLastError());
   } else {
-    size_t tb = L.tmp_bytes;
-    TV_HIP(rocprim::segmented_radix_sort_pairs_desc(w + L.tmp, tb, keys, skeys, rocprim::counting_iterator<int>(0),
-                                                    sidx, n, (unsigned)B, offs, offs + 1, 0, 32, s));
+    constexpr int lds = yolact::kSortCap * 8;
+    static std::once_flag once;
+    hipError_t attr = hipSuccess;
+    std::call_once(once, [&] {
+      attr = hipFuncSetAttribute((const void*)yolact::nms_sort, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    });
+    TV_HIP(attr);
+    hipLaunchKernelGGL(yolact::nms_sort, dim3(B), dim3(yolact::kSortThreads), lds, s, keys, A, K, skeys, sidx);
+    TV_HIP(hipGetLastError());
   }
   hipLaunchKernelGGL(yolact::nms_iou, dim3((K + yolact::kIouThreads - 1) / yolact::kIouThreads, B),
                      dim3(yolact::kIouThreads), 0, s, box, box_bstride, A, K, skeys, sidx, iou_thr, conf_thr, keep);

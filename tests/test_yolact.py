@@ -187,6 +187,28 @@ def test_gpu_large_and_degenerate_nms():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("A", [20000, 40000])
+def test_gpu_nms_streaming_sort(A):
+    """nms_sort (top_k > 1024 or > 32768 anchors, up to the full sort in rank ranges of 16384)
+    against the oracle. The anchors' confidences are spaced >= 10 ulps apart (a permuted ramp of
+    the class-1 logit): nms_keys' softmax may differ from torch's CPU one by an ulp, which would
+    swap two confidences 1 ulp apart, and the order of exactly equal ones is torch's unstable
+    CPU sort order, which the reference does not define either."""
+    from tauv_vision_amd.yolact import nms
+    g = torch.Generator().manual_seed(A)
+    logits = torch.full((1, A, 4), -10.0)
+    logits[0, :, 0] = 0.0
+    logits[0, :, 1] = torch.linspace(-5.0, 5.0, A)[torch.randperm(A, generator=g)]
+    xy = torch.rand(1, A, 2, generator=g)
+    box = torch.cat([xy, 0.02 + 0.1 * torch.rand(1, A, 2, generator=g)], -1)
+    # (> 32768 anchors: the streaming kernel even at top_k 100; top_k 17000 > 16384: two rank ranges)
+    cases = ((100, 0.5, 0.05), (3000, 0.5, 0.05), (A, 0.7, 0.0)) if A < 32768 else ((100, 0.5, 0.05), (17000, 0.7, 0.0))
+    for k, iou, conf in cases:
+        ref = ry.nms(logits, box, k, iou, conf).numpy()
+        np.testing.assert_array_equal(nms(logits.cuda(), box.cuda(), k, iou, conf).cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
 def test_gpu_box_encode_matches_reference():
     from tauv_vision_amd.yolact import YolactConfig, box_encode, box_decode
     g = golden("yolact_640x360_ar3")

@@ -317,6 +317,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_C3_NW") c3_nw_mode = v == 8 ? 8 : 0;
     else if (k == "TV_C3_HALF_COST") c3_half_cost = v;
     else if (k == "TV_SLICES") slices = std::max(1, std::min(kMaxSlices, v));
+    else if (k == "TV_SLICE_LAG") slice_lag = std::max(0, v);
     else if (k == "TV_C3_STAMPS") {  // "op:device pointer" (stamp builds of conv3x3 only)
 #if defined(TV_C3_EXP) && TV_C3_EXP == 9
       stamp_op = v;
@@ -1150,6 +1151,14 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
     const size_t in_frame = input_u8 ? (size_t)desc.in_h * desc.in_w * 3
                                      : (size_t)plan.in_channels * desc.in_h * desc.in_w * 4;
     const size_t out_frame = (size_t)plan.out_h * plan.out_w * plan.out_cpad;
+    // (diagnostic TV_SLICE_LAG = L: the other slices start once slice 0 has run its first L
+    // ops, so that their heavy first layers meet slice 0's latency-bound deep levels — measured
+    // slower: 4647 frames/s at L = 0, 4465 / 4338 / 4311 at L = 26 / 56 / 64, profiles/r4r)
+    const size_t lag = std::min((size_t)slice_lag, plan.ops.size());
+    if (lag) {
+      rc = run_all(input, input_u8, sz[0], out, s, 0, lag);
+      if (rc) return rc;
+    }
     TV_HIP(hipEventRecord(ss->fork, s));
     size_t f0 = (size_t)sz[0];
     for (size_t k = 1; k < sz.size(); ++k) {
@@ -1158,7 +1167,7 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
       if (rc) return rc;
       f0 += (size_t)sz[k];
     }
-    rc = run_all(input, input_u8, sz[0], out, s);
+    rc = run_all(input, input_u8, sz[0], out, s, lag, plan.ops.size());
     if (rc) return rc;
     for (size_t k = 1; k < sz.size(); ++k) {
       TV_HIP(hipEventRecord(ss->join[k - 1], ss->s[k - 1]));

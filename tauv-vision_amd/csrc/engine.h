@@ -97,6 +97,7 @@ struct Engine {
   static constexpr int kMaxSlices = 8;  // == TV_MAX_SLICES (include/tauv_vision_amd.h)
   int slices = 2;
   int slice_min = 8;
+  int slice_lag = 0;  // diagnostics (knob TV_SLICE_LAG): slice 1 starts after slice 0's op `slice_lag`
   std::vector<int> slice_sizes_env;
   std::vector<int> slice_sizes(int B) const;
   struct SideStreams {

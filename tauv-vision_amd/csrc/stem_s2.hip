@@ -179,6 +179,8 @@ __device__ __forceinline__ void unroll(F& f) {
   }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <typename T>
 __device__ __forceinline__ unsigned pack2(float a, float b) {
   typedef T t2 __attribute__((ext_vector_type(2)));
@@ -416,7 +418,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       }
       const int sy = 2 * oy0 + 2 * hy - P, sx = 2 * ox0 + 2 * hx - Q;
       const bool in = (unsigned)sy < (unsigned)H && (unsigned)sx < (unsigned)W;
+      const unsigned keep = in ? 0xffffffffu : 0u;  // outside the image: conv1's zero padding
       char* hdst = smem + OFF_H + (hy * RS + hx) * PITCH;
+      // bias on packed fp32 adds, ReLU, one v_cvt_pk per pair, the image mask on the packed pair
+      // (the select before the conversion split every v_cvt_pk into two converts and a pack)
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
         float v[2][4];
@@ -425,10 +430,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
           const int G2 = 2 * m + gg;
           const f32x4 bb = *reinterpret_cast<const f32x4*>(lbs + 8 * G2 + 4 * lh);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[gg][e] = in ? fmaxf(acc[4 * G2 + e] + bb[e], 0.0f) : 0.0f;
+          for (int e = 0; e < 4; e += 2) {
+            const f32x2 t = f32x2{acc[4 * G2 + e], acc[4 * G2 + e + 1]} + f32x2{bb[e], bb[e + 1]};
+            v[gg][e] = fmaxf(t[0], 0.0f);
+            v[gg][e + 1] = fmaxf(t[1], 0.0f);
+          }
         }
-        const unsigned a0 = pack2<T>(v[0][0], v[0][1]), a1 = pack2<T>(v[0][2], v[0][3]);
-        const unsigned b0 = pack2<T>(v[1][0], v[1][1]), b1 = pack2<T>(v[1][2], v[1][3]);
+        const unsigned a0 = pack2<T>(v[0][0], v[0][1]) & keep, a1 = pack2<T>(v[0][2], v[0][3]) & keep;
+        const unsigned b0 = pack2<T>(v[1][0], v[1][1]) & keep, b1 = pack2<T>(v[1][2], v[1][3]) & keep;
         const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
         const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
         if (valid) *reinterpret_cast<uint4*>(hdst + (16 * m + 8 * lh) * sizeof(T)) = make_uint4(r0[0], r1[0], r0[1], r1[1]);

@@ -107,6 +107,9 @@ constexpr int kPipeTileM = 256;
 // mode-0 k-steps only (every segment's channel count a multiple of 64 / 128 bytes)
 int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles);
 int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s);
+constexpr int kLatGroupMax = 4;  // layers per grouped conv_lat launch
+// independent layers in one launch (hp: host copies for validation, dp: their device copies)
+int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* dp, int n, int dtype, hipStream_t s);
 // fp32 slab floats one conv_lat split-K tile slice needs (64 x 128)
 constexpr int kLatSlabFloats = 64 * 128;
 
@@ -226,6 +229,9 @@ struct ConvTParams {
 bool convt_supported(int cin, int cout, int src_ldc, int add_ldc, int out_ldc);
 void convt_schedule(ConvTParams& p, int cu_count);
 int launch_convt(const ConvTParams& p, int dtype, hipStream_t s);
+constexpr int kConvTGroupMax = 4;  // up-steps per grouped convt launch
+int convt_workgroups(const ConvTParams& p);
+int launch_convt_group(const ConvTParams* const* ps, int n, int dtype, hipStream_t s);
 
 // ---- small kernels -----------------------------------------------------------------
 int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad, int dtype,

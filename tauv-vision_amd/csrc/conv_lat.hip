@@ -52,8 +52,9 @@ typedef __attribute__((address_space(1))) unsigned gu32;  // global (never flat)
 __device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
 __device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 
+// one workgroup's tile (or split-K slice of a tile) of the layer *pp; bid = its index in the layer
 template <typename T>
-__global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__ pp) {
+__device__ __forceinline__ void conv_lat_tile(const ConvParams* __restrict__ pp, const int bid) {
   const ConvParams& p = *pp;
   constexpr int VEC = 16 / sizeof(T);
   constexpr int BK = ROWB / sizeof(T);
@@ -72,7 +73,6 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
   // (split-K: the ksplit slices of a tile adjacent too, so they tend to share an XCD — speed only)
   const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
   const int nbk = p.mtiles * p.ntiles * ksplit;
-  const int bid = blockIdx.x;
   const int q8 = nbk >> 3, r8 = nbk & 7, xcd = bid & 7;
   const int lin_s = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int lin = lin_s / ksplit;      // tile
@@ -360,6 +360,34 @@ __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__
 }
 
 template <typename T>
+__global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__ pp) {
+  conv_lat_tile<T>(pp, blockIdx.x);
+}
+
+// several independent layers in one launch (the engine's schedule: layers of one dependency
+// level): workgroups [end[k-1], end[k]) run layer k, each with its own split-K slab / tickets
+struct LatGroup {
+  const ConvParams* p[kLatGroupMax];
+  int end[kLatGroupMax];
+  int n;
+};
+template <typename T>
+__global__ __launch_bounds__(NT, 1) void conv_lat_group(const LatGroup g) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < g.n && b >= g.end[k]) ++k;  // (workgroup-uniform)
+  conv_lat_tile<T>(g.p[k], b - (k ? g.end[k - 1] : 0));
+}
+
+template <typename T>
+static int launch_group_t(const LatGroup& g, hipStream_t s) {
+  if (int r = ensure_lds<conv_lat_group<T>>(LDS)) return r;
+  hipLaunchKernelGGL(conv_lat_group<T>, dim3(g.end[g.n - 1]), dim3(NT), LDS, s, g);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
+template <typename T>
 static int launch_t(const ConvParams& p, const ConvParams* dp, hipStream_t s) {
   if (int r = ensure_lds<conv_lat<T>>(LDS)) return r;
   hipLaunchKernelGGL(conv_lat<T>, dim3(p.mtiles * p.ntiles * (p.ksplit > 1 ? p.ksplit : 1)), dim3(NT), LDS, s, dp);
@@ -375,14 +403,42 @@ int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles) {
   return *mtiles * *ntiles;
 }
 
+static bool lat_geometry_ok(const ConvParams& p) {
+  return p.ks && p.nks > 0 && p.mtiles == (p.M + lat::PX - 1) / lat::PX && p.ntiles * lat::CH >= p.N && p.N % 8 == 0 &&
+         p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && p.out && !(p.ksplit > 1 && (!p.slab || !p.cnt || p.ksplit > p.nks));
+}
+
 int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s) {
-  if (!p.ks || p.nks <= 0 || p.mtiles != (p.M + lat::PX - 1) / lat::PX || p.ntiles * lat::CH < p.N || p.N % 8 ||
-      p.out_ldc % 8 || p.out_coff % 8 || !p.out || (p.ksplit > 1 && (!p.slab || !p.cnt || p.ksplit > p.nks))) {
+  if (!lat_geometry_ok(p)) {
     set_error("conv_lat: inconsistent launch geometry");
     return 1;
   }
   if (dtype == F16) return lat::launch_t<_Float16>(p, dp, s);
   if (dtype == BF16) return lat::launch_t<__bf16>(p, dp, s);
+  set_error("conv_lat: fp16/bf16 only");
+  return 1;
+}
+
+int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* dp, int n, int dtype, hipStream_t s) {
+  if (n < 1 || n > kLatGroupMax) {
+    set_error("conv_lat group: 1..kLatGroupMax layers");
+    return 1;
+  }
+  lat::LatGroup g{};
+  g.n = n;
+  int wg = 0;
+  for (int k = 0; k < n; ++k) {
+    const ConvParams& p = *hp[k];
+    if (!lat_geometry_ok(p)) {
+      set_error("conv_lat group: inconsistent launch geometry");
+      return 1;
+    }
+    wg += p.mtiles * p.ntiles * (p.ksplit > 1 ? p.ksplit : 1);
+    g.p[k] = dp[k];
+    g.end[k] = wg;
+  }
+  if (dtype == F16) return lat::launch_group_t<_Float16>(g, s);
+  if (dtype == BF16) return lat::launch_group_t<__bf16>(g, s);
   set_error("conv_lat: fp16/bf16 only");
   return 1;
 }

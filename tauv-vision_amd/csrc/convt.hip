@@ -59,15 +59,15 @@ struct ASet {
 // step in flight under the current one (NP = 4 on large inputs; NP = 1 spreads small inputs over
 // s*s times more workgroups).
 template <typename T, int NP>
-__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void convt_add(ConvTParams p) {
+__device__ __forceinline__ void convt_tile(const ConvTParams& p, const int bx) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   static_assert(NP == 1 || NP % 2 == 0, "phase group");
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, lh = lane >> 5;
-  const int group = blockIdx.x / p.nchunks;
-  const int chunk = blockIdx.x - group * p.nchunks;
+  const int group = bx / p.nchunks;
+  const int chunk = bx - group * p.nchunks;
   const int phase0 = group * NP;
 
   // ---- the group's weights and bias into LDS (rows n = phase*C + co of the packed [N][Kpad])
@@ -236,6 +236,37 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 }
 
 template <typename T, int NP>
+__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void convt_add(ConvTParams p) {
+  convt_tile<T, NP>(p, blockIdx.x);
+}
+
+// several independent up-steps in one launch (the engine's schedule: ops of one dependency level
+// on the latency path): workgroups [end[k-1], end[k]) run up-step k
+struct ConvTGroup {
+  ConvTParams p[kConvTGroupMax];
+  int end[kConvTGroupMax];
+  int n;
+};
+template <typename T, int NP>
+__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void convt_add_group(
+    const ConvTGroup g) {
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < g.n && b >= g.end[k]) ++k;  // (workgroup-uniform)
+  convt_tile<T, NP>(g.p[k], b - (k ? g.end[k - 1] : 0));
+}
+
+template <typename T, int NP>
+static int launch_group_t(const ConvTGroup& g, hipStream_t s) {
+  constexpr int lds = lds_bytes<NP>();
+  if (int r = ensure_lds<convt_add_group<T, NP>>(lds)) return r;
+  auto k = convt_add_group<T, NP>;
+  hipLaunchKernelGGL(k, dim3(g.end[g.n - 1]), dim3(NT), lds, s, g);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
+template <typename T, int NP>
 static int launch_t(const ConvTParams& p, hipStream_t s) {
   auto k = convt_add<T, NP>;
   constexpr int lds = lds_bytes<NP>();
@@ -269,6 +300,34 @@ void convt_schedule(ConvTParams& p, int cu_count) {
   if (chunks < 1) chunks = 1;
   p.nchunks = (int)chunks;
   p.tpw = (int)((mt + chunks * convt::NW - 1) / (chunks * convt::NW));  // most tiles any wave runs
+}
+
+int convt_workgroups(const ConvTParams& p) { return p.s * p.s / std::max(1, p.np) * p.nchunks; }
+
+int launch_convt_group(const ConvTParams* const* ps, int n, int dtype, hipStream_t s) {
+  using namespace convt;
+  if (n < 1 || n > kConvTGroupMax) {
+    set_error("convt group: 1..kConvTGroupMax up-steps");
+    return 1;
+  }
+  ConvTGroup g{};
+  g.n = n;
+  int wg = 0;
+  for (int k = 0; k < n; ++k) {
+    const ConvTParams& p = *ps[k];
+    if (p.tpw < 1 || p.nchunks < 1 || p.s < 1 || p.np != ps[0]->np || (p.np != 1 && p.np != NPG)) {
+      set_error("convt group: unscheduled or mixed phase groups");
+      return 1;
+    }
+    wg += convt_workgroups(p);
+    g.p[k] = p;
+    g.end[k] = wg;
+  }
+  const bool np4 = ps[0]->np == NPG;
+  if (dtype == F16) return np4 ? launch_group_t<_Float16, NPG>(g, s) : launch_group_t<_Float16, 1>(g, s);
+  if (dtype == BF16) return np4 ? launch_group_t<__bf16, NPG>(g, s) : launch_group_t<__bf16, 1>(g, s);
+  set_error("convt: fp16/bf16 only");
+  return 1;
 }
 
 int launch_convt(const ConvTParams& p, int dtype, hipStream_t s) {

@@ -50,8 +50,11 @@ struct Workspace {
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
   std::vector<ConvTParams> tparams; // per op: convt.hip launch parameters
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
-  float* slab = nullptr;            // conv_lat split-K partial tiles (ops run in order: one buffer)
-  unsigned* cnt = nullptr;          // conv_lat split-K tickets, one per tile, zeroed per forward
+  float* slab = nullptr;            // conv_lat split-K partial tiles (one region per slot of a grouped launch)
+  unsigned* cnt = nullptr;          // conv_lat split-K tickets, one per tile and slot, zeroed per forward
+  std::vector<int> level;           // per op: dependency level (the arena's time; plan order when not grouping)
+  std::vector<int> order;           // the ops in execution order: by level, then plan order
+  std::vector<std::vector<int>> groups;  // the schedule: conv_lat layers of one level in one launch, others alone
   size_t cnt_bytes = 0;
   std::vector<std::string> kname;   // per op: kernel instance name (diagnostics), filled lazily
 };
@@ -82,6 +85,8 @@ struct Engine {
                                // (env TV_LAT=0 off)
   int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (env TV_DCN64=0 off)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
+  int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)
+  int lat_group_max_b = 8;     // ... on workspaces of at most this many frames (knob TV_LATGROUP_B)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)
   int stamp_op = -1;           // diagnostics: op whose conv3x3 launch gets a stamp buffer (knob TV_C3_STAMPS=op:ptr)
   unsigned long long* stamp_buf = nullptr;

@@ -107,6 +107,9 @@ constexpr int kPipeTileM = 256;
 // mode-0 k-steps only (every segment's channel count a multiple of 64 / 128 bytes)
 int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles);
 int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s);
+// streaming stride-1 1x1 conv over concatenated inputs, weights resident in LDS (conv1x1.hip)
+bool conv1x1_stream_supported(const ConvParams& p, int esz);
+int launch_conv1x1_stream(const ConvParams& p, const ConvParams* dp, int dtype, int cu_count, hipStream_t s);
 constexpr int kLatGroupMax = 4;  // layers per grouped conv_lat launch
 // independent layers in one launch (hp: host copies for validation, dp: their device copies)
 int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* dp, int n, int dtype, hipStream_t s);

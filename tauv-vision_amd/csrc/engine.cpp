@@ -308,6 +308,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
+    else if (k == "TV_C1X1") c1x1_mode = v ? 1 : 0;
     else if (k == "TV_LATGROUP_B") lat_group_max_b = std::max(1, v);
     else if (k == "TV_DCN64") dcn64_mode = v;
     else if (k == "TV_CONVT") convt_mode = v;
@@ -917,6 +918,22 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->s2_grid[i] = 0;
     ws->lat[i] = 1;
   }
+  // stride-1 1x1 convs over concatenated inputs (the Roots) that the pipelined GEMM would run: the
+  // streaming kernel (conv1x1.hip) with the weights resident in LDS (knob TV_C1X1=0: off)
+  ws->c1x1.assign(plan.ops.size(), 0);
+  for (size_t i = 0; i < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    if (!c1x1_mode || dtype == F32 || op.kind != OP_CONV || op.up_s || op.add >= 0 || op.out < 0 || ws->lat[i] ||
+        ws->small[i] || ws->c3_tw[i] || ws->s2_grid[i] || ws->head_fused[i] || ws->head_skip[i] || ws->dcn[i].x ||
+        ws->dcn_skip[i] || (int)i == stem_op || (int)i == ss2_op || ws->convt[i])
+      continue;
+    bool one = !op.segs.empty();
+    for (const SegSpec& sg : op.segs)
+      one = one && sg.kh == 1 && sg.kw == 1 && sg.stride == 1 && sg.pad == 0 && !sg.row_expand && sg.convt_phase < 0;
+    if (!one || !conv1x1_stream_supported(ws->params[i], esz)) continue;
+    ws->c1x1[i] = 1;
+    ws->use_pipe[i] = 0;
+  }
   // conv_lat split-K over workgroups for the layers whose tiles leave most CUs idle (the latency
   // path: at B=1 every conv_lat layer is one k-step chain of ~9 latency-bound k-steps per K group):
   // up to lat_split_max workgroups per tile, each slice >= 2 k-steps (one per K group), the tiles x
@@ -1141,6 +1158,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;
   if (ws->small[i]) return launch_conv_small(p, ws->dparams + i, dtype, cu_count, s);
   if (ws->lat[i]) return launch_conv_lat(p, ws->dparams + i, dtype, s);
+  if (ws->c1x1[i]) return launch_conv1x1_stream(p, ws->dparams + i, dtype, cu_count, s);
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
                                            ws->c3_res[i], ws->c3_ni[i], ws->c3_nw[i])
@@ -1337,6 +1355,8 @@ const char* Engine::op_kernel(int B, size_t i) {
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";
       else if (ws->lat[i])
         name = std::string("tv::lat::conv_lat<") + t + ">";
+      else if (ws->c1x1[i])
+        name = std::string("tv::c1x1::conv1x1_stream<") + t + (op.N > 64 ? ", 4>" : ", 2>");
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ", " + std::to_string(ws->c3_nw[i]) + ">";
       else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";

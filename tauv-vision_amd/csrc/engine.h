@@ -45,6 +45,7 @@ struct Workspace {
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
   std::vector<int> small;           // per op: 1 = narrow-channel 3x3 conv on conv_small.hip
   std::vector<int> lat;             // per op: 1 = split-K small-level GEMM on conv_lat.hip
+  std::vector<int> c1x1;            // per op: 1 = streaming 1x1 conv (Roots) on conv1x1.hip
   std::vector<int> dcn_skip;        // per op: 1 = DCN sampling done inside the next op's fused kernel
   std::vector<DcnParams> dcn;       // per op: fused DCNv2 launch (dcn.hip) when dcn[i].x != null
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
@@ -85,6 +86,7 @@ struct Engine {
                                // (env TV_LAT=0 off)
   int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (env TV_DCN64=0 off)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
+  int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1)
   int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)
   int lat_group_max_b = 8;     // ... on workspaces of at most this many frames (knob TV_LATGROUP_B)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)

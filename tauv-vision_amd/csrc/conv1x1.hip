@@ -41,9 +41,11 @@ struct Chunk {
 };
 
 // NI = output channels / 32 (4: 128, 2: 64)
+// (N > 128: workgroup g runs the 128-channel slice g % ntiles of the output over its share of the
+// pixel tiles; the input is read once per slice)
 template <typename T, int NI>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void conv1x1_stream(
-    const ConvParams* __restrict__ pp, int wpitch) {
+    const ConvParams* __restrict__ pp, int wpitch, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ConvParams& p = *pp;
   const int tid = threadIdx.x;
@@ -52,12 +54,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int l32 = lane & 31, lh = lane >> 5;
   const int nrows = NI * 32;
   const int K = p.Kpad;  // packed row length: segment s's channels at [seg.kbase * 64, + C)
+  const int nt = blockIdx.x % ntiles, wgi = blockIdx.x / ntiles, nwg = gridDim.x / ntiles;
+  const int n0 = nt * 128, nloc = min(p.N - n0, nrows);
 
   // ---- weights [nrows][K] and bias into LDS (all loads issued before the stores)
   {
     const int cpr = K * (int)sizeof(T) / 16;  // 16-byte chunks per row
     const int total = nrows * cpr;
-    const char* wsrc = reinterpret_cast<const char*>(p.weight);
+    const char* wsrc = reinterpret_cast<const char*>(p.weight) + (size_t)n0 * K * sizeof(T);
     for (int base = 0; base < total; base += 8 * NT) {
       uint4 v[8];
 #pragma unroll
@@ -74,13 +78,13 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       }
     }
     float* lb = reinterpret_cast<float*>(smem + nrows * wpitch);
-    if (tid < nrows) lb[tid] = tid < p.N ? p.bias[tid] : 0.0f;
+    if (tid < nrows) lb[tid] = tid < nloc ? p.bias[n0 + tid] : 0.0f;
   }
   __syncthreads();
 
   const int M = p.M;
   const int mt = (M + 31) / 32;
-  const long long gw = (long long)blockIdx.x * NW + wave, nw = (long long)gridDim.x * NW;
+  const long long gw = (long long)wgi * NW + wave, nw = (long long)nwg * NW;
   const int t_begin = (int)(mt * gw / nw);
   const int t_end = (int)(mt * (gw + 1) / nw);
   if (t_begin >= t_end) return;
@@ -109,7 +113,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   auto epilogue = [&](int t) __attribute__((always_inline)) {
     const int m = t * 32 + l32;
     const bool ok = m < M;
-    T* out = reinterpret_cast<T*>(p.out) + (size_t)(ok ? m : 0) * p.out_ldc + p.out_coff;
+    T* out = reinterpret_cast<T*>(p.out) + (size_t)(ok ? m : 0) * p.out_ldc + p.out_coff + n0;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
 #pragma unroll
@@ -132,7 +136,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
         const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
         const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
         const int ch = 32 * i + 16 * mm + 8 * lh;
-        if (ok && ch < p.N) gstore16(out + ch, make_uint4(r0[0], r1[0], r0[1], r1[1]));
+        if (ok && ch < nloc) gstore16(out + ch, make_uint4(r0[0], r1[0], r0[1], r1[1]));
       }
     }
   };
@@ -181,7 +185,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 }  // namespace c1x1
 
 bool conv1x1_stream_supported(const ConvParams& p, int esz) {
-  if (esz != 2 || p.nseg < 1 || p.nseg > kMaxSeg || p.N < 8 || p.N > 128 || p.N % 8 || p.out_ldc % 8 ||
+  if (esz != 2 || p.nseg < 1 || p.nseg > kMaxSeg || p.N < 8 || p.N > 4 * 128 || p.N % 8 || p.out_ldc % 8 ||
       p.out_coff % 8 || p.Kpad > c1x1::MAXK || p.Kpad % 64 || p.up_s)
     return false;
   for (int s = 0; s < p.nseg; ++s) {
@@ -199,6 +203,7 @@ int launch_conv1x1_stream(const ConvParams& p, const ConvParams* dp, int dtype, 
     set_error("conv1x1_stream: unsupported layer");
     return 1;
   }
+  const int ntiles = (p.N + 127) / 128;
   const int ni = p.N > 64 ? 4 : 2;
   const int wpitch = p.Kpad * 2 + 16;
   const int lds = ni * 32 * wpitch + ni * 32 * 4;
@@ -207,8 +212,9 @@ int launch_conv1x1_stream(const ConvParams& p, const ConvParams* dp, int dtype, 
     return 1;
   }
   const long mt = ((long)p.M + 31) / 32;
-  const int grid = (int)std::max(1L, std::min<long>(cu_count, (mt + NW - 1) / NW));
-  using L = void (*)(const ConvParams*, int);
+  const int per = (int)std::max(1L, std::min<long>(std::max(1, cu_count / ntiles), (mt + NW - 1) / NW));
+  const int grid = per * ntiles;
+  using L = void (*)(const ConvParams*, int, int);
   L k = nullptr;
   if (dtype == F16) k = ni == 4 ? conv1x1_stream<_Float16, 4> : conv1x1_stream<_Float16, 2>;
   else if (dtype == BF16) k = ni == 4 ? conv1x1_stream<__bf16, 4> : conv1x1_stream<__bf16, 2>;
@@ -223,7 +229,7 @@ int launch_conv1x1_stream(const ConvParams& p, const ConvParams* dp, int dtype, 
     attr = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_MAX);
   });
   TV_HIP(attr);
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, wpitch);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, dp, wpitch, ntiles);
   TV_HIP(hipGetLastError());
   return 0;
 }

@@ -308,7 +308,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
-    else if (k == "TV_C1X1") c1x1_mode = v ? 1 : 0;
+    else if (k == "TV_C1X1") c1x1_mode = std::max(0, std::min(2, v));
     else if (k == "TV_LATGROUP_B") lat_group_max_b = std::max(1, v);
     else if (k == "TV_DCN64") dcn64_mode = v;
     else if (k == "TV_CONVT") convt_mode = v;
@@ -919,7 +919,8 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->lat[i] = 1;
   }
   // stride-1 1x1 convs over concatenated inputs (the Roots) that the pipelined GEMM would run: the
-  // streaming kernel (conv1x1.hip) with the weights resident in LDS (knob TV_C1X1=0: off)
+  // streaming kernel (conv1x1.hip) with the weights resident in LDS, 128 output channels per
+  // workgroup (knob TV_C1X1=0: off, 2: only layers of at most 128 output channels)
   ws->c1x1.assign(plan.ops.size(), 0);
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
@@ -930,7 +931,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
     bool one = !op.segs.empty();
     for (const SegSpec& sg : op.segs)
       one = one && sg.kh == 1 && sg.kw == 1 && sg.stride == 1 && sg.pad == 0 && !sg.row_expand && sg.convt_phase < 0;
-    if (!one || !conv1x1_stream_supported(ws->params[i], esz)) continue;
+    if (!one || !conv1x1_stream_supported(ws->params[i], esz) || (c1x1_mode == 2 && ws->params[i].N > 128)) continue;
     ws->c1x1[i] = 1;
     ws->use_pipe[i] = 0;
   }

@@ -86,7 +86,7 @@ struct Engine {
                                // (env TV_LAT=0 off)
   int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (env TV_DCN64=0 off)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
-  int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1)
+  int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1; 2 = N <= 128 only)
   int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)
   int lat_group_max_b = 8;     // ... on workspaces of at most this many frames (knob TV_LATGROUP_B)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)

@@ -47,3 +47,20 @@ def test_conv1x1_stream_matches_pipe(monkeypatch, name, precision):
         scale = max(1.0, float(ref[f].abs().max()))
         err = float((got[f] - ref[f]).abs().max())
         assert err <= tol * scale, f"{name} {precision} {f}: {err:.3e}"
+
+
+def test_wide_roots_on_conv1x1_stream(monkeypatch):
+    """DLA-34's level-4 Roots (256 output channels) run as 128-channel slices of conv1x1_stream;
+    knob TV_C1X1=2 keeps layers wider than 128 channels on conv_pipe, with the same outputs within
+    the low-precision tolerance."""
+    import test_gpu_dla34 as dla
+    builder = lambda: dla.build("b1_480x640_kp", "fp16")[0]  # noqa: E731
+    x = normalize(seeded_u8_frames(16, 480, 640, seed=17).permute(0, 3, 1, 2).float() / 255.0).cuda()
+    ref, kref = _run(monkeypatch, {"TV_C1X1": "2"}, builder, x)
+    got, kern = _run(monkeypatch, {}, builder, x)
+    wide = [lab for lab, k in kern.items() if "level4" in lab and k.startswith("tv::c1x1::")]
+    assert wide, kern
+    assert not any(kref[lab].startswith("tv::c1x1::") for lab in wide), kref
+    for f in ref:
+        scale = max(1.0, float(ref[f].abs().max()))
+        assert float((got[f] - ref[f]).abs().max()) <= dla.TOL["fp16"] * scale, f

@@ -448,6 +448,55 @@ def yolact_setup(B, precision, device, rank=0):
                 proto=proto, pview=pview, bnms=bnms, masks=masks, box_out=box_out, step=step, k=k, F=F)
 
 
+PROTO_TOL = {"fp32": 1e-4, "fp16": 8e-4, "bf16": 6e-3}  # tests/test_yolact.py: ~3x the MI355X drift
+
+
+def yolact_parity(B, precision, device, name="protonet_f256_k8_b1_69x69"):
+    """The timed protonet's kernel instances (F = 256 at fpn[0] 69x69, batch B: the engine's
+    concurrent slices) on the reference's golden input, placed at the first frame of every slice
+    among random frames, against the golden output samples and per-channel sums stored in
+    tests/golden (made by gen_golden_yolact.py from the reference Masknet, masknet.py:45-55)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    from recipe import protonet_case, protonet_inputs, protonet_sample_index
+    from tauv_vision_amd.yolact import Masknet, YolactConfig
+    c = protonet_case(name)
+    g = np.load(os.path.join(ROOT, "tests", "golden", name + ".npz"))
+    sd, x1 = protonet_inputs(c)
+    net = Masknet(YolactConfig(550, 550, (24, 48, 96, 192, 384), (1,), (0.1, 0.2), feature_depth=c["F"],
+                               n_prototype_masks=c["k"]), precision=precision)
+    net.load_state_dict(sd)
+    eng = net.engine(device, c["H"], c["W"])
+    sizes = eng.slices(B)
+    slots = [int(v) for v in np.cumsum([0] + list(sizes[:-1]))]
+    x = torch.randn((B, c["F"], c["H"], c["W"]), generator=torch.Generator().manual_seed(77))
+    for sl in slots:
+        x[sl] = x1[0]
+    y = net(x.to(device))
+    torch.cuda.synchronize()
+    idx = protonet_sample_index(c)
+    assert torch.equal(idx, torch.from_numpy(g["sample_index"]).long()), "sample recipe drifted"
+    scale = float(np.abs(g["sample"]).max())
+    res = {"max_abs_err": 0.0, "max_chan_sum_err": 0.0}
+    tol = PROTO_TOL[precision]
+    ok = True
+    for sl in slots:
+        ys = y[sl:sl + 1].cpu()
+        got = ys.contiguous().reshape(-1)[idx].numpy()
+        err = float(np.abs(got - g["sample"]).max())
+        cs = ys.double().sum(dim=(0, 2, 3)).numpy()
+        npix = ys.shape[2] * ys.shape[3]
+        cerr = np.abs(cs - g["chan_sum"])
+        bound = tol * np.abs(g["chan_sum"]) + 4 * tol * max(1.0, scale) * npix ** 0.5
+        res["max_abs_err"] = max(res["max_abs_err"], err)
+        res["max_chan_sum_err"] = max(res["max_chan_sum_err"], float(cerr.max()))
+        ok = ok and err <= tol * max(1.0, scale) and bool((cerr <= bound).all())
+    res = {k: round(v, 7) for k, v in res.items()}
+    res.update({"ref_absmax": round(scale, 5), "tol": tol, "within_tol": ok, "batch": B, "slices": sizes,
+                "frames_checked": len(slots), "samples_per_frame": int(idx.numel()),
+                "reference": f"tests/golden/{name}.npz (reference Masknet output samples + channel sums)"})
+    return res
+
+
 def run_yolact(args, world, rank, device):
     """BASELINE config 5 (YOLACT 550x550, batch 32): one step = fpn[0] [B, 256, 69, 69] resident
     in HBM -> Masknet protonet (masknet.py:8-55; F = 256, k = 8 prototypes, train.py:28-33) ->
@@ -518,6 +567,8 @@ def run_yolact(args, world, rank, device):
         t = ev0[0].elapsed_time(ev0[1])
         best_nms = t if best_nms is None else min(best_nms, t)
 
+    parity = yolact_parity(B, args.precision, device) if not args.no_extras else None
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, ROOT)
@@ -552,7 +603,7 @@ def run_yolact(args, world, rank, device):
             "e2e_tflops": round(value * flops_frame / 1e12, 2),
             "e2e_frac_of_peak": round(value * flops_frame / 1e12 / peak, 4),
             "roofline": roof, "mask_roofline": mask_roof, "nms_ms": round(best_nms, 4),
-            "detections_per_frame": round(kept / B, 2), "cpu_baseline": cpu,
+            "detections_per_frame": round(kept / B, 2), "parity": parity, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
 

@@ -248,6 +248,16 @@ int tv_diag_dcn_conv(const void* x, const void* om, int32_t B, int32_t H, int32_
                      const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, int32_t variant,
                      void* out, void* stream);
 
+/* Diagnostics (GPU tests): a Root-style 1x1 conv (dla.py:58-76: Conv2d(sum C, N, 1) over
+ * torch.cat(children, 1) + bias + activation) through conv1x1_stream, the kernel the engine runs for
+ * stride-1 1x1 layers. src[k]: compute-dtype [M][ldc[k]] pixel rows of segment k (C[k] channels,
+ * a multiple of 64); weight: host fp32 [N][sum C] in segment order; bias: host fp32 [N]; out:
+ * compute-dtype [M][out_ldc], N channels (N a multiple of 8, <= 512). TV_F16 / TV_BF16 only.
+ * Synchronous; allocates. Returns TV_EINVAL for shapes the kernel does not take. */
+int tv_diag_conv1x1(const void* const* src, const int32_t* C, const int32_t* ldc, int32_t nseg, int32_t M,
+                    const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, void* out,
+                    int32_t out_ldc, void* stream);
+
 const char* tv_last_error(void);
 const char* tv_version(void);
 

@@ -6,6 +6,8 @@
 //    skip tensor alone (dla.py:205-207 zero padding).
 #include "common.h"
 
+#include <algorithm>
+
 // expression order as the reference's torch ops (explicit __fmaf_rn where torch's CPU kernel fuses)
 #pragma clang fp contract(off)
 
@@ -206,6 +208,24 @@ int launch_leaky_inplace(float* x, size_t n, hipStream_t s) {
   const size_t n4 = n / 4;
   if (!n4) return 0;
   hipLaunchKernelGGL(leaky_inplace, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, (float4*)x, n4);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
+// zero n16 16-byte chunks. The engine's zeroing inside a forward (the fused heads' atomic target):
+// a kernel, not hipMemsetAsync — a memset node in a captured graph broke every replay after the
+// first on this ROCm (HIP's graph packet capture; tools/replay_diag3.py, tests/test_gpu_replay_b1.py)
+__global__ void fill_zero16(uint4* __restrict__ p, size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
+int launch_fill_zero(void* p, size_t bytes, hipStream_t s) {
+  if (bytes % 16 || ((uintptr_t)p & 15)) { set_error("fill_zero: 16-byte aligned whole chunks only"); return 1; }
+  const size_t n16 = bytes / 16;
+  if (!n16) return 0;
+  const size_t blocks = std::min<size_t>((n16 + 255) / 256, 4096);
+  hipLaunchKernelGGL(fill_zero16, dim3((unsigned)blocks), dim3(256), 0, s, (uint4*)p, n16);
   TV_HIP(hipGetLastError());
   return 0;
 }

@@ -174,6 +174,9 @@ int launch_train_keypoints(const uint8_t* kvalid, const long long* klabel, const
 // diag.cpp: one DeformConv2d + bias + activation through a chosen DCN kernel (GPU tests)
 int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int om_ldc, const float* weight,
                   const float* bias, int N, int act, int dtype, int variant, void* out, hipStream_t s);
+// diag.cpp: a Root-style 1x1 conv over nseg concatenated inputs through conv1x1_stream (GPU tests)
+int diag_conv1x1(const void* const* src, const int* C, const int* ldc, int nseg, int M, const float* weight,
+                 const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s);
 
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
 // output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC
@@ -244,6 +247,8 @@ int launch_prep_u8(const uint8_t* frames, int B, int H, int W, void* out, int cp
 // ToTensor + bilinear Resize (torchvision 0.15.2 tensor semantics) + Normalize of u8 HWC frames at
 // camera resolution -> normalised fp32 NCHW [B, 3, Ho, Wo] (centernet_node.py:90-92)
 int launch_preprocess_u8(const uint8_t* frames, int B, int Hs, int Ws, int Ho, int Wo, float* out, hipStream_t s);
+// zero `bytes` (a multiple of 16, 16-byte aligned) with a kernel (graph-capture safe; see aux.hip)
+int launch_fill_zero(void* p, size_t bytes, hipStream_t s);
 // leaky_relu(0.01) in place over n fp32 values (n % 4 == 0)
 int launch_leaky_inplace(float* x, size_t n, hipStream_t s);
 // fp32 NCHW [B, C, H, W] -> NHWC compute dtype with pixel stride ldc (protonet input)

@@ -131,4 +131,74 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
   return TV_OK;
 }
 
+// Root-style 1x1 conv (dla.py:58-76: Conv2d over torch.cat(children) + bias + activation) on the
+// streaming kernel the engine uses for stride-1 1x1 layers (conv1x1.hip): nseg inputs of M pixels,
+// segment k compute-dtype [M][ldc[k]] with C[k] channels; weight host fp32 [N][sum C] (the
+// concatenated input channels in segment order), bias host fp32 [N]; out compute-dtype [M][out_ldc].
+// Packed as the engine packs a Root: segment k's channels at k-step kbase[k] (128-byte k-steps).
+int diag_conv1x1(const void* const* src, const int* C, const int* ldc, int nseg, int M, const float* weight,
+                 const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s) {
+  if (!src || !C || !ldc || !weight || !bias || !out || nseg < 1 || nseg > kMaxSeg || M < 1 || N < 1 || act < 0 ||
+      act > 2 || (dtype != F16 && dtype != BF16)) {
+    set_error("diag_conv1x1: bad argument");
+    return TV_EINVAL;
+  }
+  const int esz = dtype_size(dtype);
+  const int BK = 128 / esz;
+  ConvParams p{};
+  int kbase = 0, ctot = 0;
+  for (int k = 0; k < nseg; ++k) {
+    if (!src[k] || C[k] < 1 || ldc[k] < C[k]) {
+      set_error("diag_conv1x1: bad segment");
+      return TV_EINVAL;
+    }
+    const int ks = (C[k] + BK - 1) / BK;
+    p.seg[k] = ConvSegment{src[k], 1, M, C[k], ldc[k], 1, 1, 1, 0, 0, ks, kbase};
+    kbase += ks;
+    ctot += C[k];
+  }
+  const int Kpad = kbase * BK;
+  const int Npad = (N + 127) / 128 * 128;
+  std::vector<uint8_t> hw((size_t)Npad * Kpad * esz, 0);
+  for (int n = 0; n < N; ++n) {
+    int c0 = 0;
+    for (int k = 0; k < nseg; ++k) {
+      for (int c = 0; c < C[k]; ++c)
+        put(hw, (size_t)n * Kpad + (size_t)p.seg[k].kbase * BK + c, weight[(size_t)n * ctot + c0 + c], dtype);
+      c0 += C[k];
+    }
+  }
+  std::vector<float> hb(Npad, 0.f);
+  std::memcpy(hb.data(), bias, N * sizeof(float));
+  p.nseg = nseg;
+  p.Ho = 1;
+  p.Wo = M;
+  p.M = M;
+  p.N = N;
+  p.Kpad = Kpad;
+  p.act = act;
+  p.out = out;
+  p.out_ldc = out_ldc;
+  if (!conv1x1_stream_supported(p, esz)) {
+    set_error("diag_conv1x1: shape not supported by conv1x1_stream");
+    return TV_EINVAL;
+  }
+  DevBuf dw, db, dpar;
+  TV_HIP(hipMalloc(&dw.p, hw.size()));
+  TV_HIP(hipMemcpy(dw.p, hw.data(), hw.size(), hipMemcpyHostToDevice));
+  TV_HIP(hipMalloc(&db.p, hb.size() * 4));
+  TV_HIP(hipMemcpy(db.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  p.weight = dw.p;
+  p.bias = (const float*)db.p;
+  TV_HIP(hipMalloc(&dpar.p, sizeof(ConvParams)));
+  TV_HIP(hipMemcpy(dpar.p, &p, sizeof(ConvParams), hipMemcpyHostToDevice));
+  int dev = 0, ncu = 256;
+  TV_HIP(hipGetDevice(&dev));
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+  const int rc = launch_conv1x1_stream(p, (const ConvParams*)dpar.p, dtype, ncu, s);
+  if (rc) return rc == TV_EHIP ? rc : TV_EINVAL;
+  TV_HIP(hipStreamSynchronize(s));  // the staging buffers are freed on return
+  return TV_OK;
+}
+
 }  // namespace tv

@@ -1140,7 +1140,8 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     return op.act == 2 ? launch_leaky_inplace(out, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad, s)
                        : TV_OK;
   if (ws->head_fused[i]) {
-    TV_HIP(hipMemsetAsync(out, 0, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad * sizeof(float), s));
+    int rc = launch_fill_zero(out, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad * sizeof(float), s);
+    if (rc) return rc;
     return launch_conv3x3(ws->params[i], ws->dparams + i, out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 1);
   }
   if (ws->convt[i]) {
@@ -1209,9 +1210,10 @@ int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStrea
   Workspace* ws = nullptr;
   int rc = get_workspace(B, s, &ws);
   if (rc) return rc;
-  // conv_lat split-K tickets start every forward at zero (a memset node under capture; each
-  // tile's last slice also resets its own)
-  if (ws->cnt && op0 == 0) TV_HIP(hipMemsetAsync(ws->cnt, 0, ws->cnt_bytes, s));
+  // conv_lat split-K tickets: zeroed when the workspace is made, and every tile's last-arriving
+  // slice resets its own ticket, so each complete forward leaves them all at zero for the next
+  // (no per-forward reset launch on the latency path; a memset node in a captured graph also broke
+  // the replays after the first on this ROCm: aux.hip fill_zero16)
   const size_t nops = plan.ops.size();
   if (op0 == 0 && op1 >= nops) {  // the whole forward: the schedule's groups
     for (const std::vector<int>& g : ws->groups) {
@@ -1394,6 +1396,17 @@ int Engine::profile(const void* input, int input_u8, int B, float* out, hipStrea
       TV_HIP(hipEventElapsedTime(&t, ev[k], ev[k + 1]));
       ms[i] = t;
       flops[i] = plan.ops[i].flops * B;
+    }
+    // an op fused into another launch does its FLOPs there: the stem inside stem_s2 (block0.conv1's
+    // launch), the block-diagonal 1x1 heads inside the 3x3 heads' epilogue. Their own rows launch
+    // nothing (or only an in-place activation) and report no FLOPs.
+    for (size_t i = 0; i < n && (int)i < cap; ++i) {
+      int host = -1;
+      if (ss2_op >= 0 && (int)i == stem_op) host = ss2_op;
+      else if (ws->head_skip[i] && i > 0 && ws->head_fused[i - 1]) host = (int)i - 1;
+      if (host < 0 || host >= cap) continue;
+      flops[host] += flops[i];
+      flops[i] = 0.0;
     }
     *n_ops = (int)n;
   }

@@ -5,7 +5,9 @@ share a launch (conv_lat.hip conv_lat_group, convt.hip convt_add_group), the are
 counted in levels. The same kernels run on the same data in another launch order, so every
 output must be bit-identical to the plan-order execution (diagnostic knob TV_LATGROUP=0), at
 B = 1 and 3 (R18, DLA-34) and for the protonet's ConvTranspose phase GEMMs; profile() runs the
-schedule's order one op per launch and must agree as well."""
+schedule's order one op per launch and must agree as well. B = 8 is the largest grouped workspace
+(grouped conv_lat / convt launches at their CU packing limits) and B = 16 runs as two concurrent
+8-frame slices, each on its own grouped schedule."""
 import numpy as np
 import pytest
 import torch
@@ -28,6 +30,7 @@ def _fields(pred):
 
 
 @pytest.mark.parametrize("name,B", [("r18_c128_b1_480x640", 1), ("r18_c128_b1_480x640", 3),
+                                    ("r18_c128_b1_480x640", 8), ("r18_c128_b1_480x640", 16),
                                     ("dla34:b1_480x640_kp", 1)])
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
 def test_grouped_schedule_is_bit_identical(monkeypatch, name, B, precision):

@@ -6,6 +6,8 @@ The fused launch is the default for the 128-channel "R18" in fp16 / bf16. Checke
   * it is the kernel the engine runs (per-op profile names) and the stem op launches nothing;
   * the u8 frame path (LUT staging, both the dword-aligned and the any-width loader) is bit-equal
     to the normalised fp32 NCHW path through the same fused kernel;
+  * odd H / W (97 x 129): the last halo row / column past the image, the residual copy and the
+    E expansion at the image edge;
   * against the unfused engine (diagnostic knob TV_STEMFUSE=0: stem.hip + conv3x3s2.hip + the
     residual at stride 2 from the stored stem) every Prediction tensor agrees within the
     low-precision tolerance of test_gpu_forward.py (the two differ only in conv1's fp32
@@ -47,7 +49,7 @@ def _close(a, b, tol, what):
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
-@pytest.mark.parametrize("hw,B", [((96, 128), 3), ((96, 126), 1), ((360, 640), 1)])
+@pytest.mark.parametrize("hw,B", [((96, 128), 3), ((96, 126), 1), ((97, 129), 2), ((360, 640), 1)])
 def test_fused_matches_unfused(monkeypatch, precision, hw, B):
     H, W = hw
     fr = seeded_u8_frames(B, H, W, seed=H + W)

@@ -334,3 +334,19 @@ def test_gpu_protonet_batch_consistency():
     scale = max(1.0, float(yb.abs().max()))
     for i in (0, 8, 16):
         np.testing.assert_allclose(m(x[i:i + 1]).cpu().numpy(), yb[i:i + 1].numpy(), rtol=0, atol=1e-3 * scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+def test_gpu_protonet_bench_batch_matches_reference(precision):
+    """The protonet bench.py --model yolact times (BASELINE config 5: F = 256 at the 550x550 fpn[0]
+    of 69x69, batch 32 = two concurrent 16-frame slices, the 256-channel halo convs and the
+    full-size ConvTranspose phase GEMMs of that batch) on the reference's golden input placed at the
+    first frame of each slice: output samples and per-channel sums against the reference Masknet's
+    (masknet.py:45-55; the bench line's `parity` leg runs this same function)."""
+    import bench
+    res = bench.yolact_parity(32, precision, torch.device("cuda", 0))
+    record_measurement(f"protonet/f256_69x69_b32/{precision}", res)
+    assert res["slices"] == [16, 16], res
+    assert res["frames_checked"] == 2, res
+    assert res["within_tol"], res

@@ -258,6 +258,18 @@ int tv_diag_conv1x1(const void* const* src, const int32_t* C, const int32_t* ldc
                     const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, void* out,
                     int32_t out_ldc, void* stream);
 
+/* Diagnostics (GPU tests): one conv over nseg concatenated-K segments through conv_burst, the
+ * engine's one-shot kernel for the small pyramid levels (Tree convs with the fused 1x1
+ * conv_residual dla.py:8-52, Roots dla.py:58-76, IDAUp convs dla.py:212-284). Segment k:
+ * src[k] compute-dtype NHWC [B, H, W, ldc] with geom[6k..6k+5] = H, W, C, ldc, kernel (1 or 3,
+ * padding kernel / 2), stride; a 3x3 segment must be stride 1 over the output grid. weight: host
+ * fp32 [N][K] (K segment-major, tap-major, channel-minor), bias: host fp32 [N]; out: compute-dtype
+ * [B, Ho, Wo, out_ldc]. TV_F16 / TV_BF16; TV_EINVAL for layers the kernel does not take.
+ * Synchronous; allocates. */
+int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg, int32_t B, int32_t Ho, int32_t Wo,
+                       const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, void* out,
+                       int32_t out_ldc, void* stream);
+
 const char* tv_last_error(void);
 const char* tv_version(void);
 

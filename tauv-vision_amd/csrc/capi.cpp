@@ -380,6 +380,13 @@ int tv_diag_conv1x1(const void* const* src, const int32_t* C, const int32_t* ldc
                                      (hipStream_t)stream); })
 }
 
+int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg, int32_t B, int32_t Ho, int32_t Wo,
+                       const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, void* out,
+                       int32_t out_ldc, void* stream) {
+  TV_GUARD({ return tv::diag_conv_burst(src, geom, nseg, B, Ho, Wo, weight, bias, N, act, dtype, out, out_ldc,
+                                        (hipStream_t)stream); })
+}
+
 int tv_train_heatmap(const uint8_t* valid, const int64_t* label, const float* center, int32_t B, int32_t n_objects,
                      int32_t n_labels, int32_t in_h, int32_t in_w, int32_t downsample_ratio, double sigma,
                      float* heatmap, void* stream) {

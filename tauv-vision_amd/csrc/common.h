@@ -107,6 +107,46 @@ constexpr int kPipeTileM = 256;
 // mode-0 k-steps only (every segment's channel count a multiple of 64 / 128 bytes)
 int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles);
 int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s);
+// One-shot small-level conv (conv_burst.hip): 64 output pixels (raster, one frame) x 32 channels
+// per 256-thread workgroup, K split over its 4 waves (<= 20 k-steps of 16 each, weights in
+// registers), every input the tile reads staged in LDS at once. Segments: 3x3 / stride 1 / pad 1
+// over the output grid, or 1x1 at any stride; 128-channel multiples.
+constexpr int kBurstMaxSeg = 3;
+constexpr int kBurstGroupMax = 4;  // layers per grouped launch
+struct BurstSeg {
+  const void* src;
+  int H, W, C, ldc;
+  int planes;     // C / 128
+  int kind;       // 0: 3x3 / s1 / p1 window, 1: 1x1 at `stride`
+  int stride;
+  int wrow;       // kind 0: window row pitch (pixels) = Wo + 2
+  int npix;       // staged pixels per 128-channel plane
+  int kbase16;    // first k-step (of 16) of the segment
+  int lds_off;    // staging region (bytes)
+};
+struct BurstParams {
+  BurstSeg seg[kBurstMaxSeg];
+  int nseg;
+  int B, Ho, Wo, tiles_pf, ptiles, ntiles, nk16;
+  const void* w;        // conv_burst_repack() copy
+  const float* bias;
+  int act;
+  void* out;
+  int out_ldc, out_coff, N;
+  int lds, zero_off;    // dynamic LDS bytes; the zero block's offset
+};
+struct BurstGroup {
+  BurstParams p[kBurstGroupMax];
+  int end[kBurstGroupMax];
+  int n;
+};
+// the launch geometry of a conv (p: the engine's ConvParams for a B-frame workspace); false when
+// the layer is not representable (strided 3x3, channel counts, LDS)
+bool conv_burst_plan(const ConvParams& p, int B, BurstParams* out);
+size_t conv_burst_weight_bytes(const BurstParams& p);
+int conv_burst_repack(const void* w, int Kpad, int esz, const BurstParams& p, void* out, hipStream_t s);
+int conv_burst_workgroups(const BurstParams& p);
+int launch_conv_burst(const BurstParams* const* ps, int n, int dtype, hipStream_t s);
 // streaming stride-1 1x1 conv over concatenated inputs, weights resident in LDS (conv1x1.hip)
 bool conv1x1_stream_supported(const ConvParams& p, int esz);
 int launch_conv1x1_stream(const ConvParams& p, const ConvParams* dp, int dtype, int cu_count, hipStream_t s);
@@ -177,6 +217,9 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
 // diag.cpp: a Root-style 1x1 conv over nseg concatenated inputs through conv1x1_stream (GPU tests)
 int diag_conv1x1(const void* const* src, const int* C, const int* ldc, int nseg, int M, const float* weight,
                  const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s);
+// diag.cpp: one multi-segment conv (3x3 / 1x1 segments) through conv_burst (GPU tests)
+int diag_conv_burst(const void* const* src, const int* geom, int nseg, int B, int Ho, int Wo, const float* weight,
+                    const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s);
 
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
 // output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC

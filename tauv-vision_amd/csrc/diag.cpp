@@ -201,4 +201,78 @@ int diag_conv1x1(const void* const* src, const int* C, const int* ldc, int nseg,
   return TV_OK;
 }
 
+// One conv through the one-shot small-level kernel (conv_burst.hip), packed as the engine packs a
+// multi-segment conv: segment k = a kxk (k = 1 or 3, pad k / 2) conv at `stride` over
+// src[k] (compute dtype NHWC [B, H, W, ldc], C channels); geom[6 k ..] = H, W, C, ldc, k, stride;
+// weight host fp32 [N][K], K = segment-major, tap-major, channel-minor; bias host fp32 [N];
+// out compute dtype [B, Ho, Wo, out_ldc].
+int diag_conv_burst(const void* const* src, const int* geom, int nseg, int B, int Ho, int Wo, const float* weight,
+                    const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s) {
+  if (!src || !geom || !weight || !bias || !out || nseg < 1 || nseg > kBurstMaxSeg || B < 1 || Ho < 1 || Wo < 1 ||
+      N < 1 || act < 0 || act > 2 || (dtype != F16 && dtype != BF16)) {
+    set_error("diag_conv_burst: bad argument");
+    return TV_EINVAL;
+  }
+  const int BK = 64;
+  ConvParams p{};
+  int kbase = 0;
+  std::vector<int> koff(nseg);
+  int ktot = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const int* g = geom + 6 * k;
+    const int H = g[0], W = g[1], C = g[2], ldc = g[3], kk = g[4], st = g[5];
+    if (!src[k] || H < 1 || W < 1 || C < 1 || ldc < C || (kk != 1 && kk != 3) || st < 1) {
+      set_error("diag_conv_burst: bad segment");
+      return TV_EINVAL;
+    }
+    const int ks = (kk * kk * C + BK - 1) / BK;
+    p.seg[k] = ConvSegment{src[k], H, W, C, ldc, kk, kk, st, kk / 2, kk / 2, ks, kbase};
+    koff[k] = ktot;
+    ktot += kk * kk * C;
+    kbase += ks;
+  }
+  const int Kpad = kbase * BK;
+  const int Npad = (N + 127) / 128 * 128;
+  std::vector<uint8_t> hw((size_t)Npad * Kpad * 2, 0);
+  for (int n = 0; n < N; ++n)
+    for (int k = 0; k < nseg; ++k) {
+      const int kk = geom[6 * k + 4], C = geom[6 * k + 2];
+      for (int t = 0; t < kk * kk * C; ++t)
+        put(hw, (size_t)n * Kpad + (size_t)p.seg[k].kbase * BK + t, weight[(size_t)n * ktot + koff[k] + t], dtype);
+    }
+  std::vector<float> hb(Npad, 0.f);
+  std::memcpy(hb.data(), bias, N * sizeof(float));
+  p.nseg = nseg;
+  p.Ho = Ho;
+  p.Wo = Wo;
+  p.M = B * Ho * Wo;
+  p.N = N;
+  p.Kpad = Kpad;
+  p.act = act;
+  p.out = out;
+  p.out_ldc = out_ldc;
+  DevBuf dw, db, dwb;
+  TV_HIP(hipMalloc(&dw.p, hw.size()));
+  TV_HIP(hipMemcpy(dw.p, hw.data(), hw.size(), hipMemcpyHostToDevice));
+  TV_HIP(hipMalloc(&db.p, hb.size() * 4));
+  TV_HIP(hipMemcpy(db.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+  p.weight = dw.p;
+  p.bias = (const float*)db.p;
+  BurstParams bp{};
+  if (!conv_burst_plan(p, B, &bp)) {
+    set_error("diag_conv_burst: layer not representable by conv_burst");
+    return TV_EINVAL;
+  }
+  TV_HIP(hipMalloc(&dwb.p, conv_burst_weight_bytes(bp)));
+  int rc = conv_burst_repack(dw.p, Kpad, 2, bp, dwb.p, s);
+  if (!rc) {
+    bp.w = dwb.p;
+    const BurstParams* pp = &bp;
+    rc = launch_conv_burst(&pp, 1, dtype, s);
+  }
+  if (rc) return rc == TV_EHIP ? rc : TV_EINVAL;
+  TV_HIP(hipStreamSynchronize(s));
+  return TV_OK;
+}
+
 }  // namespace tv

@@ -308,6 +308,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
+    else if (k == "TV_BURST") burst_mode = std::max(0, std::min(2, v));
     else if (k == "TV_C1X1") c1x1_mode = std::max(0, std::min(2, v));
     else if (k == "TV_LATGROUP_B") lat_group_max_b = std::max(1, v);
     else if (k == "TV_DCN64") dcn64_mode = v;
@@ -414,6 +415,7 @@ Engine::~Engine() {
     if (p.w_c3h) (void)hipFree(p.w_c3h);
     if (p.w_c3e) (void)hipFree(p.w_c3e);
     if (p.w_ss2) (void)hipFree(p.w_ss2);
+    if (p.w_burst) (void)hipFree(p.w_burst);
     if (p.head_w) (void)hipFree(p.head_w);
     if (p.head_b) (void)hipFree(p.head_b);
     if (p.bias) (void)hipFree(p.bias);
@@ -918,6 +920,32 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->s2_grid[i] = 0;
     ws->lat[i] = 1;
   }
+  // the conv_lat layers conv_burst.hip represents (every segment a 3x3 / stride 1 window or a 1x1
+  // over 128-channel multiples, K <= 1280, the staged window within LDS) take the one-shot kernel:
+  // no k-step chain, no split-K hand-off (knob TV_BURST=0 keeps them on conv_lat)
+  ws->burst.assign(plan.ops.size(), 0);
+  ws->bparams.assign(plan.ops.size(), BurstParams{});
+  for (size_t i = 0; burst_mode && i < plan.ops.size(); ++i) {
+    if (!ws->lat[i]) continue;
+    BurstParams bp{};
+    if (!conv_burst_plan(ws->params[i], B, &bp)) continue;
+    // only where every tile is resident at once with a small window: measured (profiles/r5): a
+    // second round of tiles, or one workgroup per CU for an 89 KiB 80-column window, loses to
+    // conv_lat's split-K (60x80 at B=1: 25.6 vs 16.5 us per launch; 15x20 at B=32: 16.7 vs 17 us)
+    const int per_cu = std::min(3, (160 * 1024) / std::max(1, bp.lds));
+    if (burst_mode == 1 && (bp.lds > 64 * 1024 || conv_burst_workgroups(bp) > per_cu * cu_count)) continue;
+    Packed& pk = packed[i];
+    if (!pk.w_burst) {
+      TV_HIP(hipMalloc(&pk.w_burst, conv_burst_weight_bytes(bp)));
+      int rc = conv_burst_repack(pk.w, pk.Kpad, esz, bp, pk.w_burst, nullptr);
+      if (rc) return rc;
+      TV_HIP(hipDeviceSynchronize());
+    }
+    bp.w = pk.w_burst;
+    ws->bparams[i] = bp;
+    ws->burst[i] = 1;
+    ws->lat[i] = 0;
+  }
   // stride-1 1x1 convs over concatenated inputs (the Roots) that the pipelined GEMM would run: the
   // streaming kernel (conv1x1.hip) with the weights resident in LDS, 128 output channels per
   // workgroup (knob TV_C1X1=0: off, 2: only layers of at most 128 output channels)
@@ -925,6 +953,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   for (size_t i = 0; i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     if (!c1x1_mode || dtype == F32 || op.kind != OP_CONV || op.up_s || op.add >= 0 || op.out < 0 || ws->lat[i] ||
+        ws->burst[i] ||
         ws->small[i] || ws->c3_tw[i] || ws->s2_grid[i] || ws->head_fused[i] || ws->head_skip[i] || ws->dcn[i].x ||
         ws->dcn_skip[i] || (int)i == stem_op || (int)i == ss2_op || ws->convt[i])
       continue;
@@ -968,7 +997,14 @@ int Engine::make_workspace(int B, Workspace* ws) {
     for (size_t k = 0; k < nops;) {
       const int i = ws->order[k++];
       std::vector<int> g{i};
-      if (grouping && ws->lat[i]) {
+      if (grouping && ws->burst[i]) {  // one-shot layers of one level: no CU budget (no tickets)
+        while (k < nops && (int)g.size() < kBurstGroupMax) {
+          const int j = ws->order[k];
+          if (!ws->burst[j] || ws->level[j] != ws->level[i]) break;
+          g.push_back(j);
+          ++k;
+        }
+      } else if (grouping && ws->lat[i]) {
         int used = wgs(i);
         while (k < nops && (int)g.size() < kLatGroupMax) {
           const int j = ws->order[k];
@@ -1159,6 +1195,10 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;
   if (ws->small[i]) return launch_conv_small(p, ws->dparams + i, dtype, cu_count, s);
+  if (ws->burst[i]) {
+    const BurstParams* bp = &ws->bparams[i];
+    return launch_conv_burst(&bp, 1, dtype, s);
+  }
   if (ws->lat[i]) return launch_conv_lat(p, ws->dparams + i, dtype, s);
   if (ws->c1x1[i]) return launch_conv1x1_stream(p, ws->dparams + i, dtype, cu_count, s);
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
@@ -1219,6 +1259,10 @@ int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStrea
     for (const std::vector<int>& g : ws->groups) {
       if (g.size() == 1) {
         rc = run_op((size_t)g[0], ws, input, input_u8, out, s);
+      } else if (ws->burst[g[0]]) {
+        const BurstParams* bp[kBurstGroupMax];
+        for (size_t k = 0; k < g.size(); ++k) bp[k] = &ws->bparams[g[k]];
+        rc = launch_conv_burst(bp, (int)g.size(), dtype, s);
       } else if (ws->convt[g[0]]) {
         const ConvTParams* tp[kConvTGroupMax];
         for (size_t k = 0; k < g.size(); ++k) tp[k] = &ws->tparams[g[k]];
@@ -1358,6 +1402,13 @@ const char* Engine::op_kernel(int B, size_t i) {
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";
       else if (ws->lat[i])
         name = std::string("tv::lat::conv_lat<") + t + ">";
+      else if (ws->burst[i]) {
+        const int q = (ws->bparams[i].nk16 + 3) / 4;
+        int kpw = 20;
+        for (int v : {4, 6, 8, 12, 18, 20})
+          if (q <= v) { kpw = v; break; }
+        name = std::string("tv::burst::conv_burst<") + t + ", " + std::to_string(kpw) + ">";
+      }
       else if (ws->c1x1[i])
         name = std::string("tv::c1x1::conv1x1_stream<") + t + (op.N > 64 ? ", 4>" : ", 2>");
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
@@ -1384,7 +1435,10 @@ int Engine::profile(const void* input, int input_u8, int B, float* out, hipStrea
   TV_HIP(hipEventRecord(ev[0], s));
   for (size_t k = 0; k < n; ++k) {
     rc = run_op((size_t)ws->order[k], ws, input, input_u8, out, s);
-    if (rc) break;
+    if (rc) {  // name the op (with AMD_SERIALIZE_KERNEL=3 a faulting launch reports here)
+      set_error("op " + std::to_string(ws->order[k]) + " (" + plan.ops[ws->order[k]].label + "): " + tv_last_error());
+      break;
+    }
     TV_HIP(hipEventRecord(ev[k + 1], s));
   }
   if (!rc) {

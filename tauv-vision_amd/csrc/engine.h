@@ -17,6 +17,7 @@ struct Packed {
   void* w_c3h = nullptr;   // conv3x3.hip copy for 64-channel half tiles (ni = 2)
   void* w_c3e = nullptr;   // conv3x3.hip copy for the fused-heads body when its swizzle differs (conv3x3_k16)
   void* w_ss2 = nullptr;   // stem_s2.hip k-step-ordered copy of block0.conv1's weights (made on first use)
+  void* w_burst = nullptr; // conv_burst.hip [32-channel tile][k-step][lane] copy (made on first use)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;
@@ -45,6 +46,8 @@ struct Workspace {
   std::vector<int> head_skip;       // per op: 1 = block-diagonal 1x1 heads done by the op before
   std::vector<int> small;           // per op: 1 = narrow-channel 3x3 conv on conv_small.hip
   std::vector<int> lat;             // per op: 1 = split-K small-level GEMM on conv_lat.hip
+  std::vector<int> burst;           // per op: 1 = one-shot small-level conv on conv_burst.hip
+  std::vector<BurstParams> bparams; // per op: its conv_burst launch geometry
   std::vector<int> c1x1;            // per op: 1 = streaming 1x1 conv (Roots) on conv1x1.hip
   std::vector<int> dcn_skip;        // per op: 1 = DCN sampling done inside the next op's fused kernel
   std::vector<DcnParams> dcn;       // per op: fused DCNv2 launch (dcn.hip) when dcn[i].x != null
@@ -89,6 +92,8 @@ struct Engine {
   int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1; 2 = N <= 128 only)
   int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)
   int lat_group_max_b = 8;     // ... on workspaces of at most this many frames (knob TV_LATGROUP_B)
+  int burst_mode = 1;          // conv_burst.hip for the small conv_lat layers it represents (knob TV_BURST=0 off,
+                               // 2 = every layer it represents: diagnostics / tests)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)
   int stamp_op = -1;           // diagnostics: op whose conv3x3 launch gets a stamp buffer (knob TV_C3_STAMPS=op:ptr)
   unsigned long long* stamp_buf = nullptr;

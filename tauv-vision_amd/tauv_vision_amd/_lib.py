@@ -74,6 +74,8 @@ EXPORTS = {
     "tv_diag_dcn_conv": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                           c_vp, c_vp], c_i32),
     "tv_diag_conv1x1": ([c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp], c_i32),
+    "tv_diag_conv_burst": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32,
+                            c_vp], c_i32),
     "tv_last_error": ([], ctypes.c_char_p),
     "tv_version": ([], ctypes.c_char_p),
 }

@@ -3,10 +3,12 @@ workgroup) against the reference goldens.
 
 By default the engine picks conv_lat only for layers its other kernels spread over fewer work
 units than there are CUs (the deep DLA levels). These tests force it onto every eligible layer
-(diagnostic knob TV_LAT_UNITS huge) at B = 1 and 3, so 3x3 / stride-2 / Root concatenations / the
-fused 1x1 residual / DLA-34's identity residuals all run through it at full size, and compare
-with the reference outputs at the same tolerances as the default path (test_gpu_forward.py,
-test_gpu_dla34.py).
+(diagnostic knob TV_LAT_UNITS huge, the one-shot conv_burst.hip off: TV_BURST=0) at B = 1 and 3,
+so 3x3 / stride-2 / Root concatenations / the fused 1x1 residual / DLA-34's identity residuals all
+run through it at full size, and compare with the reference outputs at the same tolerances as the
+default path (test_gpu_forward.py, test_gpu_dla34.py). By default conv_burst.hip takes the conv_lat
+layers it represents (tests/test_gpu_conv_burst.py); conv_lat keeps the strided 3x3 ones and the
+wide DLA-34 levels.
 """
 import pytest
 import torch
@@ -23,7 +25,7 @@ def _force(monkeypatch):
     """Engines built in this test get the diagnostic knob TV_LAT_UNITS (tv_engine_create_diag);
     the product path reads no environment."""
     from tauv_vision_amd import engine as E
-    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_LAT_UNITS": str(10 ** 9)})
+    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_LAT_UNITS": str(10 ** 9), "TV_BURST": "0"})
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
@@ -58,15 +60,17 @@ def test_lat_everywhere_dla34(monkeypatch, precision):
 
 
 def test_lat_default_selection_b32():
-    """At the bench's 32-frame slice the deep levels (30x40 and below) run on conv_lat and the
-    120x160 / 60x80 levels stay on the halo kernels."""
+    """At the bench's 32-frame slice the deep levels (15x20 and below) leave the halo kernels: the
+    stride-1 layers whose tiles fit one round for the one-shot conv_burst, the rest for conv_lat; the 120x160 /
+    60x80 levels stay on the halo kernels."""
     name = "r18_c128_b1_480x640"
     model, oc, mc, case = fwd.build(name, "fp16")
     eng = model.engine(torch.device("cuda", 0), 480, 640)
     frames = torch.zeros((32, 480, 640, 3), dtype=torch.uint8, device="cuda")
     kern = {label: k for label, _, _, k in eng.profile(frames, eng.alloc_out(32))}
-    assert kern["backbone.dla_down.tree_layers.2.tree_l.tree_r.conv1"].startswith("tv::lat::conv_lat<"), kern
-    assert kern["backbone.dla_down.tree_layers.4.tree_r.root.conv"].startswith("tv::lat::conv_lat<"), kern
+    assert kern["backbone.dla_down.tree_layers.2.tree_l.tree_r.conv2+conv_residual"].startswith("tv::lat::conv_lat<"), kern
+    assert kern["backbone.dla_down.tree_layers.4.tree_r.root.conv"].startswith("tv::burst::conv_burst<"), kern
+    assert kern["backbone.dla_down.tree_layers.2.tree_l.tree_l.conv1"].startswith("tv::lat::conv_lat<"), kern
     assert kern["backbone.dla_down.tree_layers.0.tree_l.tree_r.conv1"].startswith("tv::c3::conv3x3<"), kern
     assert kern["backbone.multi_ida_up.ida_up_layers.0.output_layers.0.0"].startswith("tv::c3::conv3x3<"), kern
 
@@ -79,12 +83,13 @@ def test_lat_split_k_b1(monkeypatch):
     from tauv_vision_amd import engine as E
     name = "r18_c128_b1_480x640"
     img = case_input(name).cuda()
+    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_BURST": "0"})  # every deep layer on conv_lat
     model, oc, mc, case = fwd.build(name, "fp16")
     runs = [model(img) for _ in range(3)]
     for f in ("heatmap", "size", "offset"):
         for r in runs[1:]:
             assert torch.equal(getattr(r, f), getattr(runs[0], f)), f
-    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_LAT_SPLIT": "1"})
+    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_LAT_SPLIT": "1", "TV_BURST": "0"})
     model1, _, _, _ = fwd.build(name, "fp16")
     ref = model1(img)
     g = golden(f"model_{name}")

@@ -89,6 +89,7 @@ struct ConvParams {
   const float* head_b;  // [ntiles][32] 1x1 bias on the first tile of each head, zeros elsewhere
   int head_ldc;
   int head_row0[16], head_nrows[16];
+  int head_store;       // 1: every output column written by exactly one tile -> plain stores (no zeroing)
   unsigned long long* dbg;  // diagnostic stamp builds only (conv3x3 TV_C3_EXP == 9): per-wave cycle buckets
   // conv_lat split-K over workgroups: ksplit workgroups per tile each walk a slice of the k-steps,
   // write their fp32 partial tile to slab[tile][slice] (write-through), and the last to arrive

@@ -682,13 +682,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(64 * NWV, 64 * NWV), amdgp
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const bool plain = p.head_store;  // (uniform) each output column from exactly one tile
           for (int idx = lane; idx < 32 * n; idx += 64) {
             const int px = idx / n, r = idx - px * n;
             const int qq = qf + px;
             const int yy = y0 + qq / TW, xx = x0 + qq % TW;
-            if (yy < H && xx < W && fr < nframes)
-              unsafeAtomicAdd(hout + ((size_t)(fr * H + yy) * W + xx) * p.head_ldc + 16 * hh + r,
-                              hs[px * 16 + r] + hb[16 * hh + r]);
+            if (yy < H && xx < W && fr < nframes) {
+              float* dst = hout + ((size_t)(fr * H + yy) * W + xx) * p.head_ldc + 16 * hh + r;
+              const float val = hs[px * 16 + r] + hb[16 * hh + r];
+              if (plain) *dst = 0.0f + val;  // (the atomic path's sum onto a zeroed output: 0 + v)
+              else unsafeAtomicAdd(dst, val);
+            }
           }
           // ... and those reads before the next half's / fragment's writes of the scratch
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -847,6 +847,21 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.head_row0[t] = pk2.head_row0[t];
       p.head_nrows[t] = pk2.head_nrows[t];
     }
+    // plain stores when the tiles' head rows tile the output columns exactly once (R18: one
+    // 128-channel hidden tile per head); otherwise (DLA-34: a head's 256 hidden channels span two
+    // tiles that meet in the output) atomics onto a zeroed output
+    {
+      std::vector<int> cover(plan.out_cpad, 0);
+      bool ok = true;
+      for (int t = 0; t < p.ntiles && t < 16; ++t)
+        for (int r = 0; r < p.head_nrows[t]; ++r) {
+          const int c = p.head_row0[t] + r;
+          if (c < 0 || c >= plan.out_cpad) ok = false;
+          else ++cover[c];
+        }
+      for (int c : cover) ok = ok && c == 1;
+      p.head_store = ok ? 1 : 0;
+    }
     ws->head_fused[i] = 1;
     ws->head_skip[i + 1] = 1;
   }
@@ -1176,8 +1191,10 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     return op.act == 2 ? launch_leaky_inplace(out, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad, s)
                        : TV_OK;
   if (ws->head_fused[i]) {
-    int rc = launch_fill_zero(out, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad * sizeof(float), s);
-    if (rc) return rc;
+    if (!ws->params[i].head_store) {
+      int rc = launch_fill_zero(out, (size_t)ws->B * plan.out_h * plan.out_w * plan.out_cpad * sizeof(float), s);
+      if (rc) return rc;
+    }
     return launch_conv3x3(ws->params[i], ws->dparams + i, out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 1);
   }
   if (ws->convt[i]) {

@@ -270,6 +270,17 @@ int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg
                        const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, void* out,
                        int32_t out_ldc, void* stream);
 
+/* Diagnostics (GPU tests): one ConvTranspose2d(C, N, 3, stride 2, padding 1, output_padding 1) +
+ * bias + activation (YOLACT protonet up-sampling, masknet.py:21,33) through convt3, the engine's
+ * kernel for it. src: compute-dtype NHWC [B, H, W, ldc], C channels (a multiple of 32); weight: host
+ * fp32 [C][N][3][3] (nn.ConvTranspose2d layout), N a multiple of 64; bias: host fp32 [N]; out:
+ * compute-dtype NHWC [B, 2H, 2W, out_ldc]. tile_w x tile_h: the input tile (<= 256 pixels, halo
+ * (tile_w + 1)(tile_h + 1) <= 307), 0 = the kernel's choice. TV_F16 / TV_BF16; TV_EINVAL for shapes
+ * the kernel does not take. Synchronous; allocates. */
+int tv_diag_convt3(const void* src, int32_t B, int32_t H, int32_t W, int32_t C, int32_t ldc, const float* weight,
+                   const float* bias, int32_t N, int32_t act, int32_t dtype, int32_t tile_w, int32_t tile_h, void* out,
+                   int32_t out_ldc, void* stream);
+
 const char* tv_last_error(void);
 const char* tv_version(void);
 

@@ -387,6 +387,13 @@ int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg
                                         (hipStream_t)stream); })
 }
 
+int tv_diag_convt3(const void* src, int32_t B, int32_t H, int32_t W, int32_t C, int32_t ldc, const float* weight,
+                   const float* bias, int32_t N, int32_t act, int32_t dtype, int32_t tile_w, int32_t tile_h, void* out,
+                   int32_t out_ldc, void* stream) {
+  TV_GUARD({ return tv::diag_convt3(src, B, H, W, C, ldc, weight, bias, N, act, dtype, tile_w, tile_h, out, out_ldc,
+                                    (hipStream_t)stream); })
+}
+
 int tv_train_heatmap(const uint8_t* valid, const int64_t* label, const float* center, int32_t B, int32_t n_objects,
                      int32_t n_labels, int32_t in_h, int32_t in_w, int32_t downsample_ratio, double sigma,
                      float* heatmap, void* stream) {

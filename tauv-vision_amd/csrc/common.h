@@ -222,6 +222,10 @@ int diag_conv1x1(const void* const* src, const int* C, const int* ldc, int nseg,
 int diag_conv_burst(const void* const* src, const int* geom, int nseg, int B, int Ho, int Wo, const float* weight,
                     const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s);
 
+// diag.cpp: one ConvTranspose2d(3, s2, p1, op1) + bias + activation through convt3 (GPU tests)
+int diag_convt3(const void* src, int B, int H, int W, int C, int ldc, const float* weight, const float* bias, int N,
+                int act, int dtype, int tw, int tr, void* out, int out_ldc, hipStream_t s);
+
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
 // output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC
 bool conv_small_supported(int cin, int cout, int stride, int cin_ldc, int out_ldc);
@@ -282,6 +286,25 @@ int launch_convt(const ConvTParams& p, int dtype, hipStream_t s);
 constexpr int kConvTGroupMax = 4;  // up-steps per grouped convt launch
 int convt_workgroups(const ConvTParams& p);
 int launch_convt_group(const ConvTParams* const* ps, int n, int dtype, hipStream_t s);
+
+// ConvTranspose2d(3, stride 2, padding 1, output_padding 1) + bias + activation, all four output
+// phases over one shared input halo (convt3.hip), fp16/bf16: the YOLACT protonet up-sampling.
+struct ConvT3Params {
+  const void* src;    // NHWC [B, H, W, ldc], C channels used
+  int B, H, W, C, ldc;
+  const void* w;      // convt3_pack() fragments
+  const float* bias;  // [N]
+  int act;
+  void* out;          // NHWC [B, 2H, 2W, out_ldc], N channels
+  int out_ldc, N;
+  int tw, tr;         // input tile (columns, rows); 0: convt3_tile()'s choice
+};
+void convt3_tile(int H, int W, int* tw, int* tr);
+bool convt3_supported(int C, int N, int ldc, int out_ldc, int H, int W, int esz);
+size_t convt3_weight_bytes(int C, int N);
+// host: weight [C][N][3][3] fp32 (nn.ConvTranspose2d layout) -> fragments in dtype (F16 / BF16)
+void convt3_pack(const float* w, int C, int N, int dtype, void* out);
+int launch_convt3(const ConvT3Params& p, int dtype, int cu_count, hipStream_t s);
 
 // ---- small kernels -----------------------------------------------------------------
 int launch_prep_nchw(const float* img, int B, int H, int W, void* out, int cpad, int dtype,

@@ -275,4 +275,46 @@ int diag_conv_burst(const void* const* src, const int* geom, int nseg, int B, in
   return TV_OK;
 }
 
+// One ConvTranspose2d(3, stride 2, padding 1, output_padding 1) + bias + activation through convt3.hip
+// (the engine's kernel for the protonet up-sampling, masknet.py:21,33): src compute dtype NHWC
+// [B, H, W, ldc] (C channels); weight host fp32 [C][N][3][3] (nn.ConvTranspose2d layout); bias host
+// fp32 [N]; out compute dtype NHWC [B, 2H, 2W, out_ldc]; (tw, tr) the input tile (0: the launch's choice).
+int diag_convt3(const void* src, int B, int H, int W, int C, int ldc, const float* weight, const float* bias, int N,
+                int act, int dtype, int tw, int tr, void* out, int out_ldc, hipStream_t s) {
+  if (!src || !weight || !bias || !out || B < 1 || H < 1 || W < 1 || act < 0 || act > 2 ||
+      (dtype != F16 && dtype != BF16) || !convt3_supported(C, N, ldc, out_ldc, H, W, 2)) {
+    set_error("diag_convt3: bad argument or shape not supported by convt3");
+    return TV_EINVAL;
+  }
+  std::vector<uint8_t> hw(convt3_weight_bytes(C, N));
+  convt3_pack(weight, C, N, dtype, hw.data());
+  DevBuf dw, db;
+  TV_HIP(hipMalloc(&dw.p, hw.size()));
+  TV_HIP(hipMemcpy(dw.p, hw.data(), hw.size(), hipMemcpyHostToDevice));
+  TV_HIP(hipMalloc(&db.p, (size_t)N * 4));
+  TV_HIP(hipMemcpy(db.p, bias, (size_t)N * 4, hipMemcpyHostToDevice));
+  ConvT3Params p{};
+  p.src = src;
+  p.B = B;
+  p.H = H;
+  p.W = W;
+  p.C = C;
+  p.ldc = ldc;
+  p.w = dw.p;
+  p.bias = (const float*)db.p;
+  p.act = act;
+  p.out = out;
+  p.out_ldc = out_ldc;
+  p.N = N;
+  p.tw = tw;
+  p.tr = tr;
+  int dev = 0, ncu = 256;
+  TV_HIP(hipGetDevice(&dev));
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+  const int rc = launch_convt3(p, dtype, ncu, s);
+  if (rc) return rc == TV_EHIP ? rc : TV_EINVAL;
+  TV_HIP(hipStreamSynchronize(s));  // the staging buffers are freed on return
+  return TV_OK;
+}
+
 }  // namespace tv

@@ -199,6 +199,16 @@ int Engine::pack_op(size_t oi) {
                   hw[(size_t)co * pk.Kpad + (size_t)kb * BK + (size_t)t * cs + ci] =
                       w[(((size_t)(sg.ci0 + ci) * wN + co) * 3 + ky) * 3 + kx];
             }
+          // all four phases in one launch (convt3.hip): the phase-(0,0) op carries the whole
+          // ConvTranspose2d's weight in that kernel's fragment order (knob TV_CT3=0: off)
+          if (ct3_mode && dtype != F32 && sg.convt_phase == 0 && op.segs.size() == 1 && sg.ci0 == 0 &&
+              sg.cin == cs && wcin == cs && convt3_supported(cs, wN, cs, wN, 1, 1, esz)) {
+            std::vector<uint8_t> frag(convt3_weight_bytes(cs, wN));
+            convt3_pack(w, cs, wN, dtype, frag.data());
+            TV_HIP(hipMalloc(&pk.w_ct3, frag.size()));
+            TV_HIP(hipMemcpy(pk.w_ct3, frag.data(), frag.size(), hipMemcpyHostToDevice));
+            weight_bytes += frag.size();
+          }
           kb += pk.seg_ksteps[si];
           continue;
         }
@@ -308,6 +318,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
+    else if (k == "TV_CT3") ct3_mode = v ? 1 : 0;
     else if (k == "TV_BURST") burst_mode = std::max(0, std::min(2, v));
     else if (k == "TV_C1X1") c1x1_mode = std::max(0, std::min(2, v));
     else if (k == "TV_LATGROUP_B") lat_group_max_b = std::max(1, v);
@@ -416,6 +427,7 @@ Engine::~Engine() {
     if (p.w_c3e) (void)hipFree(p.w_c3e);
     if (p.w_ss2) (void)hipFree(p.w_ss2);
     if (p.w_burst) (void)hipFree(p.w_burst);
+    if (p.w_ct3) (void)hipFree(p.w_ct3);
     if (p.head_w) (void)hipFree(p.head_w);
     if (p.head_b) (void)hipFree(p.head_b);
     if (p.bias) (void)hipFree(p.bias);
@@ -897,6 +909,44 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->convt[i] = 1;
     ws->use_pipe[i] = 0;
   }
+  // ConvTranspose2d(3, s2, p1, op1) as its four consecutive phase ops (protonet): one convt3.hip
+  // launch from the phase-(0,0) op over the shared input halo; the other three launch nothing
+  ws->ct3.assign(plan.ops.size(), 0);
+  ws->ct3p.assign(plan.ops.size(), ConvT3Params{});
+  for (size_t i = 0; i + 3 < plan.ops.size(); ++i) {
+    const OpSpec& op = plan.ops[i];
+    if (!packed[i].w_ct3 || op.kind != OP_CONV || op.segs.size() != 1 || op.segs[0].convt_phase != 0 ||
+        op.up_s != 2 || op.out < 0 || op.add >= 0)
+      continue;
+    bool ok = true;
+    for (int ph = 1; ph < 4; ++ph) {
+      const OpSpec& o = plan.ops[i + ph];
+      ok = ok && o.kind == OP_CONV && o.segs.size() == 1 && o.segs[0].convt_phase == ph &&
+           o.segs[0].src == op.segs[0].src && o.out == op.out && o.up_s == 2 && o.act == op.act && o.add < 0;
+    }
+    const TensorSpec& src = plan.tensors[op.segs[0].src];
+    const TensorSpec& tgt = plan.tensors[op.out];
+    ok = ok && tgt.H == 2 * src.H && tgt.W == 2 * src.W && op.N == tgt.C &&
+         convt3_supported(src.C, op.N, src.C, tgt.C, src.H, src.W, esz);
+    if (!ok) continue;
+    ConvT3Params& t = ws->ct3p[i];
+    t.src = base + ws->off[op.segs[0].src];
+    t.B = B;
+    t.H = src.H;
+    t.W = src.W;
+    t.C = src.C;
+    t.ldc = src.C;
+    t.w = packed[i].w_ct3;
+    t.bias = packed[i].bias;
+    t.act = op.act;
+    t.out = base + ws->off[op.out];
+    t.out_ldc = tgt.C;
+    t.N = op.N;
+    convt3_tile(t.H, t.W, &t.tw, &t.tr);
+    ws->ct3[i] = 1;
+    for (int ph = 0; ph < 4; ++ph) ws->use_pipe[i + ph] = 0;
+    for (int ph = 1; ph < 4; ++ph) ws->ct3[i + ph] = 2;
+  }
   // layers the chosen kernel spreads over fewer work units than the threshold (the deep pyramid
   // levels: a few 512-pixel tiles on 256 CUs) -> conv_lat.hip (small tiles, K split over waves)
   ws->lat.assign(plan.ops.size(), 0);
@@ -1207,6 +1257,8 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
                                    op.cov_y1, op.cov_x0, op.cov_x1, dtype, s);
     return TV_OK;
   }
+  if (ws->ct3[i] == 2) return TV_OK;  // a ConvTranspose2d phase done by the phase-(0,0) op's launch
+  if (ws->ct3[i]) return launch_convt3(ws->ct3p[i], dtype, cu_count, s);
   ConvParams p = ws->params[i];
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
@@ -1401,6 +1453,8 @@ const char* Engine::op_kernel(int B, size_t i) {
              t + ">";
     if (name.empty()) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
+      else if (ws->ct3[i] == 1) name = std::string("tv::ct3::convt3<") + t + ">";
+      else if (ws->ct3[i] == 2) name = "(fused into the phase (0,0) launch: convt3)";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->dcn_skip[i]) name = "(sampled inside the fused DCNv2 kernel)";
       else if (ws->dcn[i].x) {
@@ -1475,6 +1529,7 @@ int Engine::profile(const void* input, int input_u8, int B, float* out, hipStrea
       int host = -1;
       if (ss2_op >= 0 && (int)i == stem_op) host = ss2_op;
       else if (ws->head_skip[i] && i > 0 && ws->head_fused[i - 1]) host = (int)i - 1;
+      else if (ws->ct3[i] == 2) host = (int)i - plan.ops[i].segs[0].convt_phase;
       if (host < 0 || host >= cap) continue;
       flops[host] += flops[i];
       flops[i] = 0.0;

@@ -18,6 +18,7 @@ struct Packed {
   void* w_c3e = nullptr;   // conv3x3.hip copy for the fused-heads body when its swizzle differs (conv3x3_k16)
   void* w_ss2 = nullptr;   // stem_s2.hip k-step-ordered copy of block0.conv1's weights (made on first use)
   void* w_burst = nullptr; // conv_burst.hip [32-channel tile][k-step][lane] copy (made on first use)
+  void* w_ct3 = nullptr;   // convt3.hip fragments of a whole ConvTranspose2d(3, s2) (its phase-(0,0) op)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
   std::vector<int> seg_ksteps;
@@ -53,6 +54,9 @@ struct Workspace {
   std::vector<DcnParams> dcn;       // per op: fused DCNv2 launch (dcn.hip) when dcn[i].x != null
   std::vector<int> convt;           // per op: 1 = OP_CONVT_ADD on convt.hip
   std::vector<ConvTParams> tparams; // per op: convt.hip launch parameters
+  std::vector<int> ct3;             // per op: 1 = ConvTranspose2d(3, s2) phase (0,0) launching all four on convt3.hip,
+                                    // 2 = a phase that launch covers
+  std::vector<ConvT3Params> ct3p;   // per op: convt3.hip launch parameters (ct3 == 1)
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
   float* slab = nullptr;            // conv_lat split-K partial tiles (one region per slot of a grouped launch)
   unsigned* cnt = nullptr;          // conv_lat split-K tickets, one per tile and slot, zeroed per forward
@@ -92,6 +96,7 @@ struct Engine {
   int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1; 2 = N <= 128 only)
   int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)
   int lat_group_max_b = 8;     // ... on workspaces of at most this many frames (knob TV_LATGROUP_B)
+  int ct3_mode = 1;            // ConvTranspose2d(3, s2, p1) phases in one convt3.hip launch (knob TV_CT3=0 off)
   int burst_mode = 1;          // conv_burst.hip for the small conv_lat layers it represents (knob TV_BURST=0 off,
                                // 2 = every layer it represents: diagnostics / tests)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)

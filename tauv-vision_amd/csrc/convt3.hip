@@ -42,9 +42,15 @@ constexpr int WPIECES = NQ * (NCO / 16);      // 36 fragments of 1 KiB per chann
 constexpr int WBUF = WPIECES * 1024;
 constexpr int OFF_W = 2 * HBUF;
 constexpr int OFF_B = OFF_W + 2 * WBUF;
-constexpr int LDS = OFF_B + NCO * 4;
+constexpr int LDS = OFF_B + 2 * NCO * 4;  // (a bias slot per buffer set)
 static_assert(LDS <= 160 * 1024, "LDS budget");
 constexpr int OOB = (int)0x80000000u;
+#ifndef CT3_WD
+#define CT3_WD 8   // weight fragments in flight per wave (ring depth)
+#endif
+#ifndef CT3_SCHED
+#define CT3_SCHED 1
+#endif
 
 // (phase, tap) q: the phase p = 2 pi + pj and the tap t = 2 dy + dx it multiplies; the order the
 // packed weights use (taps grouped: tap 0 serves all 4 phases, taps 1 / 2 two, tap 3 one)
@@ -94,7 +100,7 @@ __device__ __forceinline__ unsigned pack2(float a, float b) {
 template <int V>
 using IC = std::integral_constant<int, V>;
 
-template <typename T>
+template <typename T, int ACT>
 __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void convt3(ConvT3Params p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef __attribute__((address_space(3))) char lds_char;
@@ -150,24 +156,44 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     if (s5_k[k] == 4 || hy_k[k] > tr) hy_k[k] = -1;
   }
   const i32x4 wrs = rsrc_of(p.w, (unsigned)(nco * ncb * WBUF));
-  // stage (unit u, channel block cb) into buffer set bs: the halo pieces, then the weight pieces
-  auto stage = [&](int u, int cb, int bs, bool first_stage = false) __attribute__((always_inline)) {
-    (void)first_stage;
+  const i32x4 brs = rsrc_of(p.bias, (unsigned)(p.N * 4));
+  // a unit's staging geometry, computed once per unit: the frame's buffer resource, this lane's
+  // byte offsets of its 3 halo chunks at channel block 0 (OOB outside the frame / halo), the
+  // weight and bias bases of its channel tile
+  struct Geo {
+    i32x4 rs;
+    int hoff[3];
+    int wblk0, boff;
+  };
+  auto geo = [&](int u) __attribute__((always_inline)) {
     int fr, y0, x0, co;
     unit_of(u, fr, y0, x0, co);
-    const i32x4 rs = rsrc_of(reinterpret_cast<const char*>(p.src) + (size_t)fr * frame_bytes, frame_bytes);
+    Geo g;
+    g.rs = rsrc_of(reinterpret_cast<const char*>(p.src) + (size_t)fr * frame_bytes, frame_bytes);
+#pragma unroll
+    for (int k = 0; k < HPIECES / NW; ++k) {
+      const int y = y0 + hy_k[k], x = x0 + hx_k[k];
+      const bool ok = hy_k[k] >= 0 && y < H && x < W;
+      g.hoff[k] = ok ? (int)((((unsigned)y * W + x) * p.ldc + s5_k[k] * 8) * sizeof(T)) : OOB;
+    }
+    g.wblk0 = co * ncb * WBUF;
+    g.boff = (co * NCO + lane) * 4;
+    return g;
+  };
+  // stage (unit geometry g, channel block cb) into buffer set bs: the halo pieces, the weight
+  // pieces, with a unit's last block its biases
+  auto stage = [&](const Geo& g, int cb, int bs, bool first_stage = false) __attribute__((always_inline)) {
+    (void)first_stage;
 #pragma unroll
     for (int k = 0; k < HPIECES / NW; ++k) {
       const int q = wave + k * NW;
-      const int y = y0 + hy_k[k], x = x0 + hx_k[k];
-      const bool ok = hy_k[k] >= 0 && y < H && x < W;
-      const int off = ok ? (int)((((unsigned)y * W + x) * p.ldc + cb * 32 + s5_k[k] * 8) * sizeof(T)) : OOB;
 #if defined(TV_CT3_EXP) && (TV_CT3_EXP == 2 || TV_CT3_EXP == 3)
       if (!first_stage) continue;  // timing experiment: stale halo
 #endif
-      raw_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(lds + bs * HBUF + q * 1024), 16, off, 0, 0, 0);
+      raw_buffer_load_lds(g.rs, (__attribute__((address_space(3))) void*)(lds + bs * HBUF + q * 1024), 16,
+                          g.hoff[k] + cb * 32 * (int)sizeof(T), 0, 0, 0);
     }
-    const int wblk = (co * ncb + cb) * WBUF;
+    const int wblk = g.wblk0 + cb * WBUF;
 #pragma unroll
     for (int k = 0; k < (WPIECES + NW - 1) / NW; ++k) {
       const int q = wave + k * NW;
@@ -178,6 +204,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       raw_buffer_load_lds(wrs, (__attribute__((address_space(3))) void*)(lds + OFF_W + bs * WBUF + q * 1024), 16,
                           wblk + q * 1024 + lane * 16, 0, 0, 0);
     }
+    // (the slot's next fill is two stages later, past a barrier)
+    if (cb == ncb - 1 && wave == 0)
+      raw_buffer_load_lds(brs, (__attribute__((address_space(3))) void*)(lds + OFF_B + bs * NCO * 4), 4, g.boff, 0, 0,
+                          0);
   };
 
   f32x4 acc[4][4][2];  // [phase][16-channel fragment][pixel fragment]
@@ -197,37 +227,45 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   }
   const unsigned tapoff[4] = {0u, (unsigned)PITCH, (unsigned)(HS * PITCH), (unsigned)((HS + 1) * PITCH)};
 
-  // one channel block from buffer set bs: 4 taps x their phases
+  // one channel block from buffer set bs: the 4 taps' input fragments up front, then the 36
+  // weight fragments in packing order (q-major: tap 0's four phases first) through a ring of
+  // WD registers, each read WD fragments (2 WD MFMAs) ahead of its use; the schedule barriers keep
+  // the compiler from sinking the reads next to their MFMAs (LDS latency exposed per pair)
   auto block = [&](int bs) __attribute__((always_inline)) {
     const unsigned hb = lds0 + (unsigned)(bs * HBUF);
     const unsigned wb = lds0 + (unsigned)(OFF_W + bs * WBUF) + (unsigned)lane * 16u;
-    auto tap = [&](auto tc) __attribute__((always_inline)) {
-      constexpr int TP = decltype(tc)::value;
-      u32x4 X[2];
+    constexpr int WD = CT3_WD;
+    u32x4 X[4][2], Wr[WD];
 #pragma unroll
-      for (int f = 0; f < 2; ++f) X[f] = lds16(hb + xrel[f] + tapoff[TP]);
+    for (int i = 0; i < WD; ++i) Wr[i] = lds16(wb + (unsigned)(i * 1024));
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if (Q_TAP[q] != TP) continue;
-        u32x4 Wf[4];
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) Wf[c] = lds16(wb + (unsigned)((q * 4 + c) * 1024));
+      for (int f = 0; f < 2; ++f) X[t][f] = lds16(hb + xrel[f] + tapoff[t]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+    for (int i = 0; i < WPIECES; ++i) {
+      const int q = i >> 2, c = i & 3;
+      const u32x4 wf = Wr[i % WD];
+      if (i + WD < WPIECES) Wr[i % WD] = lds16(wb + (unsigned)((i + WD) * 1024));
 #pragma unroll
-          for (int f = 0; f < 2; ++f) {
+      for (int f = 0; f < 2; ++f) {
 #if defined(TV_CT3_EXP) && TV_CT3_EXP == 4
-            acc[Q_PH[q]][c][f][0] += __builtin_bit_cast(float, Wf[c][0] ^ X[f][1]);  // timing experiment: no MFMA
+        acc[Q_PH[q]][c][f][0] += __builtin_bit_cast(float, wf[0] ^ X[Q_TAP[q]][f][1]);  // timing experiment: no MFMA
 #else
-            Mf<T>::run(acc[Q_PH[q]][c][f], Wf[c], X[f]);
+        Mf<T>::run(acc[Q_PH[q]][c][f], wf, X[Q_TAP[q]][f]);
 #endif
-          }
       }
-    };
-    tap(IC<0>{});
-    tap(IC<1>{});
-    tap(IC<2>{});
-    tap(IC<3>{});
+    }
+#if CT3_SCHED
+    // order: the WD + 8 prologue reads, then per fragment (one read, two MFMAs), then the last MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, WD + 8, 0);
+#pragma unroll
+    for (int i = 0; i < WPIECES - WD; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * WD, 0);
+#endif
   };
 
   // bias + activation + 16-byte stores of the unit's 4 phases (conv3x3.hip epilogue16 layout:
@@ -236,10 +274,10 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   const int cofs16 = 16 * (c16 & 1) + 8 * (c16 >> 1);
   const int tH = 2 * H, tW = 2 * W;
   const unsigned out_frame = (unsigned)tH * tW * p.out_ldc * (unsigned)sizeof(T);
-  auto epilogue = [&](int u) __attribute__((always_inline)) {
+  auto epilogue = [&](int u, int bs) __attribute__((always_inline)) {
     int fr, y0, x0, co;
     unit_of(u, fr, y0, x0, co);
-    const float* lb = reinterpret_cast<const float*>(smem + OFF_B);
+    const float* lb = reinterpret_cast<const float*>(smem + OFF_B + bs * NCO * 4);
     const i32x4 ors = rsrc_of(reinterpret_cast<const char*>(p.out) + (size_t)fr * out_frame, out_frame);
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
@@ -258,8 +296,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
               float t = acc[ph][2 * j + hh][f][e] + bb[e];
-              if (p.act == 1) t = fmaxf(t, 0.0f);
-              else if (p.act == 2) t = fmaxf(t, 0.01f * t);
+              if constexpr (ACT == 1) t = fmaxf(t, 0.0f);
+              else if constexpr (ACT == 2) t = fmaxf(t, 0.01f * t);
               v[hh][e] = t;
             }
           }
@@ -275,15 +313,14 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   };
 
   // ---- the unit list: stage (first, 0); per block stage the next (block or unit) under compute
-  stage(first, 0, 0, true);
+  Geo gcur = geo(first);
+  stage(gcur, 0, 0, true);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int bs = 0;
   for (int u = first; u < end; u += stride) {
-    int fr, y0, x0, co;
-    unit_of(u, fr, y0, x0, co);
-    // the unit's bias (read in the epilogue, after the unit's last barrier)
-    float bias_v = tid < NCO ? p.bias[co * NCO + tid] : 0.f;
+    const bool more = u + stride < end;
+    const Geo gnext = geo(more ? u + stride : u);
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph)
 #pragma unroll
@@ -291,28 +328,35 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 #pragma unroll
         for (int f = 0; f < 2; ++f) acc[ph][c][f] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int cb = 0; cb < ncb; ++cb) {
-      if (cb + 1 < ncb) stage(u, cb + 1, bs ^ 1);
-      else if (u + stride < end) stage(u + stride, 0, bs ^ 1);
+      if (cb + 1 < ncb) stage(gcur, cb + 1, bs ^ 1);
+      else if (more) stage(gnext, 0, bs ^ 1);
       block(bs);
+      // (raw barriers: __syncthreads()'s fence would wait for every outstanding store)
       if (cb + 1 == ncb) {
-        // the previous unit's epilogue read the bias: every wave is past it (barriers since)
-        if (tid < NCO) reinterpret_cast<float*>(smem + OFF_B)[tid] = bias_v;
-        __syncthreads();
-        epilogue(u);
+        epilogue(u, bs);
+        // the next stage's LDS-DMA (issued before the epilogue's 16 stores) has landed once at most
+        // the 16 stores are outstanding (vector memory ops retire in issue order): the stores
+        // drain under the next unit's first block instead of stalling this barrier
+        asm volatile("s_waitcnt vmcnt(16) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
       bs ^= 1;
     }
+    gcur = gnext;
   }
 }
 
-template <typename T>
-static int launch_t(const ConvT3Params& p, int grid, hipStream_t s) {
-  if (int r = ensure_lds<convt3<T>>(LDS)) return r;
-  hipLaunchKernelGGL(convt3<T>, dim3(grid), dim3(NT), LDS, s, p);
+template <typename T, int ACT>
+static int launch_a(const ConvT3Params& p, int grid, hipStream_t s) {
+  if (int r = ensure_lds<convt3<T, ACT>>(LDS)) return r;
+  hipLaunchKernelGGL((convt3<T, ACT>), dim3(grid), dim3(NT), LDS, s, p);
   TV_HIP(hipGetLastError());
   return 0;
+}
+template <typename T>
+static int launch_t(const ConvT3Params& p, int grid, hipStream_t s) {
+  return p.act == 1 ? launch_a<T, 1>(p, grid, s) : p.act == 2 ? launch_a<T, 2>(p, grid, s) : launch_a<T, 0>(p, grid, s);
 }
 
 }  // namespace ct3
@@ -384,7 +428,7 @@ int launch_convt3(const ConvT3Params& p_in, int dtype, int cu_count, hipStream_t
     return 1;
   }
   if (!convt3_supported(p.C, p.N, p.ldc, p.out_ldc, p.H, p.W, dtype_size(dtype)) || !p.src || !p.w || !p.out ||
-      !p.bias || p.B < 1 || p.H < 1 || p.W < 1) {
+      !p.bias || p.B < 1 || p.H < 1 || p.W < 1 || p.act < 0 || p.act > 2) {
     set_error("convt3: unsupported layer");
     return 1;
   }

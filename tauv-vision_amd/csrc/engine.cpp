@@ -1453,7 +1453,7 @@ const char* Engine::op_kernel(int B, size_t i) {
              t + ">";
     if (name.empty()) {
       if (ws->convt[i]) name = std::string("tv::convt::convt_add<") + t + ", " + std::to_string(ws->tparams[i].np) + ">";
-      else if (ws->ct3[i] == 1) name = std::string("tv::ct3::convt3<") + t + ">";
+      else if (ws->ct3[i] == 1) name = std::string("tv::ct3::convt3<") + t + ", " + std::to_string(ws->ct3p[i].act) + ">";
       else if (ws->ct3[i] == 2) name = "(fused into the phase (0,0) launch: convt3)";
       else if (ws->head_skip[i]) name = "(fused into the 3x3 heads)";
       else if (ws->dcn_skip[i]) name = "(sampled inside the fused DCNv2 kernel)";

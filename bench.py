@@ -80,8 +80,11 @@ class Pipeline:
         C, H, W = self.pred.heatmap.shape[1:]
         self.dec = DeviceDecoder(B, C, H, W, K, device)
         self.mc, self.thr, self.B = mc, thr, B
-        self.host = torch.empty((B, K, 10), dtype=torch.float32, pin_memory=True)
-        self.host_counts = torch.empty((B,), dtype=torch.int32, pin_memory=True)
+        # pinned mirror of the decoder's packed records + counts (one D2H copy per step)
+        self.host_packed = torch.empty(self.dec.packed.numel(), dtype=torch.uint8, pin_memory=True)
+        nrec = B * K * 10 * 4
+        self.host = self.host_packed[:nrec].view(torch.float32).view(B, K, 10)
+        self.host_counts = self.host_packed[nrec:].view(torch.int32)
 
     def decode(self):
         p = self.pred
@@ -95,8 +98,11 @@ class Pipeline:
     def finish(self, rec, cnt, gather=None):
         if gather is not None:
             gather(rec, cnt)  # every rank's records into the gather buffers (RCCL all-gather)
-        self.host.copy_(rec, non_blocking=True)
-        self.host_counts.copy_(cnt, non_blocking=True)
+        if rec.data_ptr() == self.dec.records.data_ptr() and cnt.data_ptr() == self.dec.counts.data_ptr():
+            self.host_packed.copy_(self.dec.packed, non_blocking=True)
+        else:  # (gathered records: separate buffers)
+            self.host.copy_(rec, non_blocking=True)
+            self.host_counts.copy_(cnt, non_blocking=True)
 
     def step(self, frames, gather=None):
         rec, cnt = self.compute(frames)

@@ -161,8 +161,9 @@ int tv_index_split(const int32_t* flat, int32_t B, int32_t K, int32_t H, int32_t
  * heatmap view and of the [B,H,W,ch] size/offset/depth views (depth may be NULL).
  * aux (may be NULL): pair gathered per record at element (b, label, j, y, x) with
  * aux_strides[5] (the [B,K,2,H,W] keypoint_affinity view).
- * workspace: tv_decode_workspace_size() bytes of device memory (any contents; it carries the
- * per-tile peak keys between the call's two launches — one call at a time per workspace). */
+ * workspace: tv_decode_workspace_size() bytes of device memory, ZERO-FILLED before its first use
+ * (it carries the per-image peak keys and the arrival counters of the call's single launch, which
+ * leaves the counters at zero again for the next call) — one call at a time per workspace. */
 int tv_decode_workspace_size(int32_t B, int32_t C, int32_t H, int32_t W, int32_t K, int64_t* bytes);
 int tv_decode(const float* heat, const int64_t heat_strides[4], const float* size, const int64_t size_strides[4],
               const float* offset, const int64_t offset_strides[4], const float* depth,

@@ -25,6 +25,23 @@
 
 namespace tv {
 
+// diagnostic builds only (EXTRA=-DTV_DEC_STAMPS=1): thread 0's shader-clock stamps at the decode
+// kernel's phase boundaries, written by the selecting workgroup into its image's last two records
+#if defined(TV_DEC_STAMPS)
+#define DSTAMP(arr, i)                                                                   \
+  do {                                                                                   \
+    if (threadIdx.x == 0) {                                                              \
+      unsigned long long t_;                                                             \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");      \
+      (arr)[i] = t_;                                                                     \
+    }                                                                                    \
+  } while (0)
+#else
+#define DSTAMP(arr, i) \
+  do {                 \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ---- heatmap_nms as a dense map (tv_heatmap_nms) ----------------------------------------
@@ -357,61 +374,93 @@ struct MergeOut {
   int records;         // 1: also write detection records (DecodeParams)
 };
 
+// A detection record's inputs, gathered from its key (decode.py:204-234 / 71-98 field meaning):
+// issued before the key's rank is known, so the loads overlap the ranking
+struct RecIn {
+  float sz0, sz1, of0, of1, d, a0, a1;
+};
+__device__ __forceinline__ RecIn gather_record(uint64_t key, int b, const DecodeParams& p) {
+  RecIn r;
+  const int idx = (int)(0xFFFFFFFFu - (uint32_t)key);
+  const int hw = p.H * p.W;
+  const int label = idx / hw;
+  const int rem = idx - label * hw;
+  const int iy = rem / p.W;
+  const int ix = rem - iy * p.W;
+  const float* sz = p.size + b * p.size_st[0] + iy * p.size_st[1] + ix * p.size_st[2];
+  r.sz0 = sz[0];
+  r.sz1 = sz[p.size_st[3]];
+  r.of0 = r.of1 = 0.f;
+  if (p.pos_mode == 0) {
+    const float* of = p.offset + b * p.offset_st[0] + iy * p.offset_st[1] + ix * p.offset_st[2];
+    r.of0 = of[0];
+    r.of1 = of[p.offset_st[3]];
+  }
+  r.d = p.depth ? p.depth[b * p.depth_st[0] + iy * p.depth_st[1] + ix * p.depth_st[2]] : 0.f;
+  r.a0 = r.a1 = __builtin_nanf("");
+  if (p.aux) {
+    const float* a = p.aux + b * p.aux_st[0] + label * p.aux_st[1] + iy * p.aux_st[3] + ix * p.aux_st[4];
+    r.a0 = a[0];
+    r.a1 = a[p.aux_st[2]];
+  }
+  return r;
+}
+
+// output slot i (rank i, descending) of image b from its key (and, for records, its gathered
+// inputs): score / flat index and / or the detection record; returns score >= threshold
+__device__ __forceinline__ int store_record(uint64_t key, const RecIn& in, int i, int K, int b, const MergeOut& mo,
+                                            const DecodeParams& p) {
+  const float score = unorder_bits((uint32_t)(key >> 32));
+  const int idx = (int)(0xFFFFFFFFu - (uint32_t)key);
+  if (mo.score) {
+    mo.score[(size_t)b * K + i] = score;
+    mo.index[(size_t)b * K + i] = idx;
+  }
+  if (!mo.records) return 0;
+  const int hw = p.H * p.W;
+  const int label = idx / hw;
+  const int rem = idx - label * hw;
+  const int iy = rem / p.W;
+  const int ix = rem - iy * p.W;
+  float* rr = p.records + ((size_t)b * K + i) * 10;
+  float y, x;
+  if (p.pos_mode == 0) {
+    y = (float)(((double)p.ratio * (double)iy + (double)in.of0) / (double)p.in_h);
+    x = (float)(((double)p.ratio * (double)ix + (double)in.of1) / (double)p.in_w);
+  } else {
+    y = (float)iy / (float)p.out_h;
+    x = (float)ix / (float)p.out_w;
+  }
+  float depth = __builtin_nanf("");
+  if (p.depth) {
+    const float sg = 1.0f / (1.0f + expf(-in.d));
+    depth = p.depth_mode == 0 ? (1.0f / sg) - 1.0f : 1.0f / sg;
+  }
+  rr[0] = (float)label;
+  rr[1] = score;
+  rr[2] = y;
+  rr[3] = x;
+  rr[4] = in.sz0;
+  rr[5] = in.sz1;
+  rr[6] = depth;
+  rr[7] = (float)idx;
+  rr[8] = in.a0;
+  rr[9] = in.a1;
+  return score >= p.score_thr ? 1 : 0;
+}
+
+__device__ __forceinline__ int write_record(uint64_t key, int i, int K, int b, const MergeOut& mo,
+                                            const DecodeParams& p) {
+  return store_record(key, mo.records ? gather_record(key, b, p) : RecIn{}, i, K, b, mo, p);
+}
+
 // top[0..K) (descending keys) -> score / flat index and, for tv_decode, the detection records
-// (decode.py:204-234 / 71-98 field meaning) + the count of scores >= threshold
+// + the count of scores >= threshold
 template <int NT>
 __device__ void write_outputs(const uint64_t* top, int K, int b, const MergeOut& mo, const DecodeParams& p,
                               int& cnt_thr) {
   int local_thr = 0;
-  for (int i = threadIdx.x; i < K; i += NT) {
-    const uint64_t key = top[i];
-    const float score = unorder_bits((uint32_t)(key >> 32));
-    const int idx = (int)(0xFFFFFFFFu - (uint32_t)key);
-    if (mo.score) {
-      mo.score[(size_t)b * K + i] = score;
-      mo.index[(size_t)b * K + i] = idx;
-    }
-    if (!mo.records) continue;
-    // detection record (decode.py:204-234 / 71-98 field meaning)
-    const int hw = p.H * p.W;
-    const int label = idx / hw;
-    const int rem = idx - label * hw;
-    const int iy = rem / p.W;
-    const int ix = rem - iy * p.W;
-    float* rr = p.records + ((size_t)b * K + i) * 10;
-    const float* sz = p.size + b * p.size_st[0] + iy * p.size_st[1] + ix * p.size_st[2];
-    float y, x;
-    if (p.pos_mode == 0) {
-      const float* of = p.offset + b * p.offset_st[0] + iy * p.offset_st[1] + ix * p.offset_st[2];
-      y = (float)(((double)p.ratio * (double)iy + (double)of[0]) / (double)p.in_h);
-      x = (float)(((double)p.ratio * (double)ix + (double)of[p.offset_st[3]]) / (double)p.in_w);
-    } else {
-      y = (float)iy / (float)p.out_h;
-      x = (float)ix / (float)p.out_w;
-    }
-    float depth = __builtin_nanf("");
-    if (p.depth) {
-      const float d = p.depth[b * p.depth_st[0] + iy * p.depth_st[1] + ix * p.depth_st[2]];
-      const float sg = 1.0f / (1.0f + expf(-d));
-      depth = p.depth_mode == 0 ? (1.0f / sg) - 1.0f : 1.0f / sg;
-    }
-    rr[0] = (float)label;
-    rr[1] = score;
-    rr[2] = y;
-    rr[3] = x;
-    rr[4] = sz[0];
-    rr[5] = sz[p.size_st[3]];
-    rr[6] = depth;
-    rr[7] = (float)idx;
-    if (p.aux) {
-      const float* a = p.aux + b * p.aux_st[0] + label * p.aux_st[1] + iy * p.aux_st[3] + ix * p.aux_st[4];
-      rr[8] = a[0];
-      rr[9] = a[p.aux_st[2]];
-    } else {
-      rr[8] = rr[9] = __builtin_nanf("");
-    }
-    local_thr += score >= p.score_thr ? 1 : 0;
-  }
+  for (int i = threadIdx.x; i < K; i += NT) local_thr += write_record(top[i], i, K, b, mo, p);
   if (mo.records) {
     if (local_thr) atomicAdd(&cnt_thr, local_thr);
     __syncthreads();
@@ -469,32 +518,58 @@ __global__ __launch_bounds__(NT) void merge_select(const uint64_t* __restrict__ 
 }
 
 
-// ---- decode fast path: peak_scan + peak_select (tv_decode: sigmoid, 3x3 NMS, records) ---------
+// ---- decode fast path: one launch (tv_decode: sigmoid, 3x3 NMS, exact top-K, records) ---------
 // The per-tile block selects above cost ~20 barriers per tile and per merge level; the decode
-// path instead makes one pass over the heatmap that keeps only what the exact top-K can need:
-//  peak_scan   : grid B x tiles. Tile + halo -> LDS (sigmoid once), NMS keys in registers; the
-//                keys of the "positive" class (score > +0, the only class the top K draws from
-//                while an image has >= K of them) are compacted into the tile's own segment of
-//                the workspace, with the tile's count. No atomics: every workgroup owns its slot.
-//  peak_select : grid B. A 12-bit radix pass over the image's positive keys (LDS histogram of
-//                the top bits, then of the next 12 bits inside the threshold bucket, ...) until
-//                at most kRankCap keys can still be in the top K; those are ranked exactly (keys
-//                are unique) into descending order and the records written. An image with
-//                fewer than K positive keys (degenerate: scores saturated to 0, NaN maps) takes
-//                an exact streaming block select over all of its keys instead.
+// path instead makes one pass over the heatmap that keeps only what the exact top-K can need, and
+// the image's last tile to finish selects:
+//  peak_scan : grid B x tiles. Tile + halo -> LDS (sigmoid once), NMS keys in registers; the keys
+//              of the "positive" class (score > +0, the only class the top K draws from while an
+//              image has >= K of them) that can still be in the tile's top K (an 8-bit digit
+//              pre-filter) are appended to the image's key array (one atomic per workgroup for the
+//              base) with write-through stores; then one agent-scope ticket per workgroup. The
+//              workgroup drawing the image's last ticket selects (fused_select): 8-bit radix
+//              passes over the image's keys (LDS histogram, one bin per thread) until at most
+//              kRankCap keys can still be in the top K; those are ranked exactly (keys are unique)
+//              into descending order and the records written. An image with fewer than K
+//              positive keys (degenerate: scores saturated to 0, NaN maps) takes an exact
+//              streaming block select over all of its keys instead. The last workgroup leaves the
+//              image's key count and ticket at zero for the next call (the workspace starts
+//              zero-filled), so a captured graph replays without a reset launch.
 constexpr int kScanThreads = 256, kScanPer = 16;
-constexpr int kScanElems = kScanThreads * kScanPer;   // 4096 elements per tile (and segment slots)
-constexpr int kHistBits = 12, kHistBins = 1 << kHistBits;
+constexpr int kScanElems = kScanThreads * kScanPer;   // 4096 elements per tile (and key slots per tile)
 constexpr int kRankCap = 256;                         // candidates ranked directly (or K when larger)
-constexpr int kMaxScanTiles = 4096;                   // tiles per image (LDS segment table of peak_select)
+constexpr int kMaxScanTiles = 4096;                   // tiles per image
 constexpr uint64_t kZeroKey = (0x80000000ull << 32) | 0xFFFFFFFFull;  // largest key of score +0.0
 
 struct ScanWs {
-  uint32_t* cnt;    // [B][tiles]   positive keys per tile
-  uint64_t* keys;   // [B][tiles][kScanElems]
-  int tiles;        // per image
-  uint32_t N;       // C * H * W
+  uint32_t* img_cnt;  // [B] keys appended so far (zero between calls)
+  uint32_t* ticket;   // [B] tiles finished (zero between calls)
+  uint64_t* keys;     // [B][tiles * kScanElems] the image's appended keys
+  int tiles;          // per image
+  uint32_t N;         // C * H * W
 };
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ void raw_buffer_store_v2(u32x2 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v2i32");
+__device__ u32x2 raw_buffer_load_v2(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v2i32");
+constexpr int kSC1 = 16;  // aux cache bits: sc1 (write-through store / L1- and L2-coherent load)
+typedef __attribute__((address_space(1))) uint32_t gu32;
+
+// the image's key array as a buffer resource (keys at 8-byte offsets)
+__device__ __forceinline__ i32x4 keys_rsrc(const ScanWs& w, int b) {
+  const unsigned long long a = (unsigned long long)(w.keys + (size_t)b * w.tiles * kScanElems);
+  i32x4 r;
+  r.x = (int)(unsigned)a;
+  r.y = (int)(unsigned)(a >> 32);
+  r.z = (int)((unsigned)w.tiles * kScanElems * 8u);
+  r.w = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ uint64_t load_key(const i32x4& rs, int i) {
+  const u32x2 v = raw_buffer_load_v2(rs, i * 8, 0, kSC1);
+  return ((uint64_t)v.y << 32) | v.x;
+}
 
 // Wave-aggregated append: the lanes with `pred` get consecutive slots of *counter (one LDS
 // atomic per wave). Call from wave-uniform control flow.
@@ -539,19 +614,263 @@ __device__ __forceinline__ int fdiv(int n, int d, float inv) {
   return q;
 }
 
+// key of flat element e of image b, recomputed from the heatmap exactly as peak_scan / tile_select
+// form it (fallback path)
+__device__ uint64_t nms_key_global(const float* base, int64_t s1, int64_t s2, int64_t s3, int H, int W, uint32_t e) {
+  const int hw = H * W;
+  const int c = (int)(e / (uint32_t)hw);
+  const int rem = (int)e - c * hw;
+  const int y = rem / W, x = rem - (rem / W) * W;
+  const float* pc = base + (int64_t)c * s1;
+  const float v = sigmoidf_ref(pc[(int64_t)y * s2 + (int64_t)x * s3]);
+  float m = v;
+  for (int dy = -1; dy <= 1; ++dy)
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int yy = y + dy, xx = x + dx;
+      const float u = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? sigmoidf_ref(pc[(int64_t)yy * s2 + (int64_t)xx * s3])
+                                                               : -INFINITY;
+      m = fmaxf(m, u);
+    }
+  return make_key((float)(m == v) * v, e);
+}
+
+// The image's last-arriving scan workgroup: exact top K of its n appended positive keys (rank
+// order = descending key) -> records (write_outputs). NT threads; NT == 256: one histogram bin
+// per thread.
+template <int NT>
+__device__ void fused_select(const i32x4 krs, int n, int b, const float* __restrict__ heat,
+                             int64_t s0, int64_t s1, int64_t s2, int64_t s3, int H, int W, int K, uint32_t N,
+                             SelectShared& sh, char* lds, int* ncand, int* cnt_thr, const MergeOut& mo,
+                             const DecodeParams& p, unsigned long long* stamps) {
+  (void)stamps;
+  static_assert(NT == 256, "one digit bin per thread");
+  int P = 1;
+  while (P < K) P <<= 1;
+  uint64_t* top = reinterpret_cast<uint64_t*>(lds);  // P keys (fallback path)
+  uint64_t* cand = top + (P < 2 ? 2 : P);             // <= max(K, kRankCap) candidates (+ a pad), 16-B aligned
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int KPT = 16;  // keys per thread when the image's keys fit in registers
+  if (tid == 0) { *ncand = 0; *cnt_thr = 0; }
+  if (n >= K) {
+    const bool cached = n <= KPT * NT;
+    uint64_t rk[KPT];
+    if (cached) {
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const int i = tid + j * NT;
+        rk[j] = i < n ? load_key(krs, i) : 0ull;
+      }
+    }
+    // every key (wave-uniform calls): registers, or the array in global memory
+    auto for_each_key = [&](auto&& f) __attribute__((always_inline)) {
+      if (cached) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) f(rk[j], tid + j * NT < n);
+      } else {
+        for (int i0 = 0; i0 < n; i0 += NT) {
+          const int i = i0 + tid;
+          f(i < n ? load_key(krs, i) : 0ull, i < n);
+        }
+      }
+    };
+    const int cap = K > kRankCap ? K : kRankCap;
+    uint64_t prefix = 0, pmask = 0;
+    int need = K, above = 0;
+    for (;;) {
+      // the keys still in play share (key & pmask) == prefix: their range, then the 8-bit digit
+      // just below the bits they all share
+      uint64_t lo = ~0ull, hi = 0;
+      int dummy = 0;
+      for_each_key([&](uint64_t key, bool valid) {
+        if (valid && (key & pmask) == prefix) {
+          lo = key < lo ? key : lo;
+          hi = key > hi ? key : hi;
+        }
+      });
+      block_minmax_sum<NT>(lo, hi, dummy, sh);
+      DSTAMP(stamps, 6);
+      if (lo == hi) {  // one key in play (need == 1): it is the threshold
+        prefix = hi;
+        pmask = ~0ull;
+        break;
+      }
+      const int msb = 63 - __builtin_clzll(lo ^ hi);
+      const int shift = msb > 7 ? msb - 7 : 0;
+      pmask |= shift + 8 >= 64 ? 0 : ~((1ull << (shift + 8)) - 1);
+      prefix = hi & pmask;
+      sh.hist[tid] = 0;
+      __syncthreads();
+      for_each_key([&](uint64_t key, bool valid) {
+        const bool in = valid && (key & pmask) == prefix;
+        hist_add(reinterpret_cast<uint32_t*>(sh.hist), in ? (uint32_t)(key >> shift) & 255u : 0u, in);
+      });
+      __syncthreads();
+      // thread t owns digit 255 - t; running count from the top
+      const int c = sh.hist[255 - tid];
+      int incl = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(incl, o);
+        if (lane >= o) incl += u;
+      }
+      if (lane == 63) sh.red_n[wave] = incl;
+      __syncthreads();
+      int before = incl - c;
+#pragma unroll
+      for (int i = 0; i < NT / 64; ++i) before += i < wave ? sh.red_n[i] : 0;
+      if (before < need && need <= before + c) {
+        sh.sel_digit = 255 - tid;
+        sh.sel_above = before;
+        sh.sel_count = c;
+      }
+      __syncthreads();
+      const int d = sh.sel_digit, a = sh.sel_above, bc = sh.sel_count;
+      __syncthreads();
+      prefix |= (uint64_t)d << shift;
+      pmask |= 255ull << shift;
+      need -= a;
+      above += a;
+      if (above + bc <= cap || shift == 0) break;
+    }
+    DSTAMP(stamps, 7);
+    // candidates: every key at or above the threshold bucket (above + its count, <= cap)
+    if (cached) {
+      // wave counts -> wave offsets (one barrier), then ballot positions (ballots recomputed:
+      // no 16 x 64-bit masks held across the barrier)
+      int wc = 0;
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) wc += (int)__popcll(__ballot(tid + j * NT < n && (rk[j] & pmask) >= prefix));
+      if (lane == 0) sh.red_n[wave] = wc;
+      __syncthreads();
+      int pos = 0;
+#pragma unroll
+      for (int i = 0; i < NT / 64; ++i) pos += i < wave ? sh.red_n[i] : 0;
+      if (tid == NT - 1) *ncand = pos + wc;
+      const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+      for (int j = 0; j < KPT; ++j) {
+        const bool in = tid + j * NT < n && (rk[j] & pmask) >= prefix;
+        const uint64_t bal = __ballot(in);
+        if (in) cand[pos + (int)__popcll(bal & lt)] = rk[j];
+        pos += (int)__popcll(bal);
+      }
+    } else {
+      __syncthreads();  // (ncand zeroed)
+      for_each_key([&](uint64_t key, bool valid) {
+        const bool in = valid && (key & pmask) >= prefix;
+        const int slot = wave_append_slot(ncand, in);
+        if (in) cand[slot] = key;
+      });
+    }
+    __syncthreads();
+    DSTAMP(stamps, 8);
+    const int m = *ncand;
+    // each candidate's rank = the candidates above it (keys are unique); ranks below K write
+    // their output slot directly
+    int local_thr = 0;
+    if (m <= NT) {
+      // one owner thread per candidate: its record inputs gathered first (the loads run under
+      // the ranking), its rank from 16-byte LDS reads (two keys each; an odd count padded with a
+      // zero key, below every real one)
+      if (tid == 0 && (m & 1)) cand[m] = 0;
+      const uint64_t mykey = tid < m ? cand[tid] : 0;
+      const RecIn in = tid < m && mo.records ? gather_record(mykey, b, p) : RecIn{};
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (the pad key)
+      int r = 0;
+      const int m2 = (m + 1) >> 1;
+      typedef const __attribute__((address_space(3))) ulonglong2 lds_u2;
+      const ulonglong2* c2 = reinterpret_cast<const ulonglong2*>(cand);
+#pragma unroll 8
+      for (int j = 0; j < m2; ++j) {
+        const ulonglong2 v = c2[j];
+        r += (v.x > mykey ? 1 : 0) + (v.y > mykey ? 1 : 0);
+      }
+      (void)sizeof(lds_u2);
+      if (tid < m && r < K) local_thr += store_record(mykey, in, r, K, b, mo, p);
+    } else {
+      for (int ci = tid; ci < m; ci += NT) {
+        const uint64_t mykey = cand[ci];
+        int r = 0;
+#pragma unroll 8
+        for (int j = 0; j < m; ++j) r += cand[j] > mykey ? 1 : 0;
+        if (r < K) local_thr += write_record(mykey, r, K, b, mo, p);
+      }
+    }
+    DSTAMP(stamps, 9);
+    if (mo.records) {
+      if (local_thr) atomicAdd(cnt_thr, local_thr);
+      // (a raw barrier: __syncthreads()'s fence would wait for every record store)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (tid == 0) p.counts[b] = *cnt_thr;
+    }
+  } else {
+    // fewer positive keys than K: exact streaming select over every key of the image (the top
+    // so far rides along in CARRY slots per thread: kMaxK keys over NT threads)
+    constexpr int CARRY = (kMaxK + NT - 1) / NT, PER = 12 + CARRY, CH = 12 * NT;
+    const float* base = heat + b * s0;
+    int have = 0;
+    for (uint32_t e0 = 0; e0 < N; e0 += CH) {
+      uint64_t k[PER];
+      int loc = 0;
+#pragma unroll
+      for (int j = 0; j < 12; ++j) {
+        const uint32_t e = e0 + tid + j * NT;
+        k[j] = e < N ? nms_key_global(base, s1, s2, s3, H, W, e) : 0;
+        loc += k[j] != 0;
+      }
+#pragma unroll
+      for (int j = 0; j < CARRY; ++j) {
+        const int i = tid + j * NT;
+        k[12 + j] = i < have ? top[i] : 0;
+        loc += k[12 + j] != 0;
+      }
+      const int real = block_count_real<NT>(loc, sh);
+      const int kt = min(K, real);
+      const uint64_t T2 = block_select<NT, PER>(k, kt, sh);
+      if (tid == 0) sh.nout = 0;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < PER; ++j)
+        if (k[j] != 0 && k[j] >= T2) top[atomicAdd(&sh.nout, 1)] = k[j];
+      __syncthreads();
+      have = kt;
+    }
+    for (int i = have + tid; i < P; i += NT) top[i] = 0;
+    __syncthreads();
+    bitonic_desc<NT>(top, P);
+    write_outputs<NT>(top, K, b, mo, p, *cnt_thr);
+  }
+  DSTAMP(stamps, 10);
+#if defined(TV_DEC_STAMPS)
+  if (threadIdx.x == 0)
+    for (int i = 1; i <= 10; ++i)
+      p.records[((size_t)b * K + K - 2) * 10 + (i - 1)] = (float)(long long)(stamps[i] - stamps[0]);
+#endif
+}
+
 // Tile element (cc, yy, xx) at image (c0 + cc, y0 + yy, x0 + xx); per-image offsets fit 32 bits
 // (launch_decode checks). CHAN_FAST: LDS fill order channel-fastest (1: NHWC views, whose
 // channels of a pixel are adjacent; 2: the same with 4 unit-stride 16-byte-aligned channels,
 // one float4 per pixel) or column-fastest (0: NCHW).
 template <int CHAN_FAST>
-__global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restrict__ heat, int64_t s0, int s1, int s2,
+// (5 workgroups per CU: <= 96 VGPRs, and the LDS of the R18 head tile fits 5 x 32 KiB)
+__global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void peak_scan(const float* __restrict__ heat, int64_t s0, int s1, int s2,
                                                            int s3, int C, int H, int W, int K, const TileGeom g,
-                                                           const ScanWs w) {
+                                                           const ScanWs w, const MergeOut mo, const DecodeParams p) {
   extern __shared__ __attribute__((aligned(16))) float tile[];
   __shared__ uint32_t wsum[kScanThreads / 64 + 1];
-  __shared__ uint32_t fhist[256];
   __shared__ int red_n[kScanThreads / 64];
   __shared__ int keep_digit;
+  __shared__ uint32_t keep_cnt, seg_base, last_flag;
+  __shared__ SelectShared ssh;
+  __shared__ int ncand, cnt_thr;
+  uint32_t* fhist = reinterpret_cast<uint32_t*>(ssh.hist);  // (the select's histogram, later)
+#if defined(TV_DEC_STAMPS)
+  __shared__ unsigned long long stamps[12];
+#else
+  unsigned long long* stamps = nullptr;
+#endif
+  DSTAMP(stamps, 0);
   const int b = blockIdx.y;
   int t = blockIdx.x;
   const int tx = t % g.ntw; t /= g.ntw;
@@ -627,6 +946,7 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
       if (dst[j] >= 0) tile[dst[j]] = inb[j] ? sigmoidf_ref(v[j]) : -INFINITY;
   }
   __syncthreads();
+  DSTAMP(stamps, 1);
 
   // NMS keys over strips of 4 columns (strip q = tid + j * NT: column-strip fastest, then row,
   // then channel): the 3 x 6 window is read once per strip; per element the same fmaxf order
@@ -696,6 +1016,7 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
       if (k[j]) *d++ = k[j];
   }
   __syncthreads();
+  DSTAMP(stamps, 2);
   // per-tile pre-filter: every key of the image's top K is among its tile's top K, so when the
   // tile has more than K keep only those whose 8-bit score digit (just below the score bits all
   // the tile's keys share) reaches the digit of the tile's K-th largest — K plus at most one
@@ -746,15 +1067,25 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
       int before = inc2 - c;
 #pragma unroll
       for (int i = 0; i < kScanThreads / 64; ++i) before += i < wave ? red_n[i] : 0;
-      if (before < K && K <= before + c) keep_digit = 255 - (int)threadIdx.x;
+      if (before < K && K <= before + c) {
+        keep_digit = 255 - (int)threadIdx.x;
+        keep_cnt = (uint32_t)(before + c);  // the keys whose digit reaches it
+      }
       __syncthreads();
       kd = (uint32_t)keep_digit;
     }
   }
-  // the kept keys -> the tile's segment (ballot positions), and the count
-  const size_t seg = (size_t)b * w.tiles + blockIdx.x;
-  uint64_t* dst = w.keys + seg * kScanElems;
-  uint32_t pos = 0;
+  DSTAMP(stamps, 3);
+  // the kept keys -> the image's key array at a base drawn with one atomic (ballot positions),
+  // write-through stores (read by whichever workgroup of the image finishes last)
+  if (threadIdx.x == 0) {
+    const uint32_t kept = kd ? keep_cnt : nk;
+    seg_base = kept ? __hip_atomic_fetch_add((gu32*)(w.img_cnt + b), kept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : 0u;
+  }
+  __syncthreads();
+  const i32x4 krs = keys_rsrc(w, b);
+  uint32_t pos = seg_base;
   const uint64_t lt = (1ull << lane) - 1;
   for (uint32_t i0 = 0; i0 < nk; i0 += kScanThreads) {
     const uint32_t i = i0 + threadIdx.x;
@@ -769,284 +1100,35 @@ __global__ __launch_bounds__(kScanThreads) void peak_scan(const float* __restric
       wo += w2 < wave ? wsum[w2] : 0u;
       tot += wsum[w2];
     }
-    if (keep) dst[pos + wo + (uint32_t)__popcll(bal & lt)] = key;
+    if (keep)
+      raw_buffer_store_v2(u32x2{(uint32_t)key, (uint32_t)(key >> 32)}, krs,
+                          (int)((pos + wo + (uint32_t)__popcll(bal & lt)) * 8u), 0, kSC1);
     pos += tot;
-    __syncthreads();
+    // (raw barriers: the stores drain once, at the hand-off below)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  if (threadIdx.x == 0) w.cnt[seg] = pos;
-}
-
-// key of flat element e of image b, recomputed from the heatmap exactly as peak_scan / tile_select
-// form it (fallback path)
-__device__ uint64_t nms_key_global(const float* base, int64_t s1, int64_t s2, int64_t s3, int H, int W, uint32_t e) {
-  const int hw = H * W;
-  const int c = (int)(e / (uint32_t)hw);
-  const int rem = (int)e - c * hw;
-  const int y = rem / W, x = rem - (rem / W) * W;
-  const float* pc = base + (int64_t)c * s1;
-  const float v = sigmoidf_ref(pc[(int64_t)y * s2 + (int64_t)x * s3]);
-  float m = v;
-  for (int dy = -1; dy <= 1; ++dy)
-    for (int dx = -1; dx <= 1; ++dx) {
-      const int yy = y + dy, xx = x + dx;
-      const float u = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? sigmoidf_ref(pc[(int64_t)yy * s2 + (int64_t)xx * s3])
-                                                               : -INFINITY;
-      m = fmaxf(m, u);
-    }
-  return make_key((float)(m == v) * v, e);
-}
-
-// Block scan of per-thread digit counts, top-down: thread t holds the counts of digits
-// D - 1 - 4t - i (i = 0..3). Leaves in `sh` the digit where the running count from the top
-// reaches `need`, the count above it and its own count.
-template <int NT>
-__device__ void topdown_pick(const uint32_t (&c)[4], int D, int need, SelectShared& sh) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int sum = (int)(c[0] + c[1] + c[2] + c[3]);
-  int incl = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(incl, o);
-    if (lane >= o) incl += u;
-  }
-  if (lane == 63) sh.red_n[wave] = incl;
+  // hand-off (cdna_hip_programming.md §6 Guideline 16, write-through form): every storing wave
+  // drains its stores, the barrier orders them before ONE relaxed agent-scope ticket; the
+  // workgroup drawing the image's last ticket selects from sc1 loads and resets the count and
+  // the ticket for the next call
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int before = incl - sum + wave_excl_prefix(sh.red_n, wave);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int d = D - 1 - 4 * (int)threadIdx.x - i;
-    if (d >= 0 && before < need && need <= before + (int)c[i]) {
-      sh.sel_digit = d;
-      sh.sel_above = before;
-      sh.sel_count = (int)c[i];
-    }
-    before += (int)c[i];
-  }
+  DSTAMP(stamps, 4);
+  if (threadIdx.x == 0)
+    last_flag = __hip_atomic_fetch_add((gu32*)(w.ticket + b), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-}
-
-constexpr int kSelThreads = 1024;
-
-__global__ __launch_bounds__(kSelThreads) void peak_select(const float* __restrict__ heat, int64_t s0, int64_t s1,
-                                                             int64_t s2, int64_t s3, int H, int W, int K,
-                                                             const ScanWs w, const MergeOut mo, const DecodeParams p) {
-  __shared__ SelectShared sh;
-  // top / cand / lh, aliased by the key-index -> segment map while the keys are loaded
-  __shared__ __attribute__((aligned(16))) char pool[2 * kMaxK * 8 + kHistBins * 4];
-  __shared__ uint32_t tcnt[kMaxScanTiles];  // segment starts (exclusive prefix of the tile counts)
-  __shared__ int cnt_thr, ncand;
-  uint64_t* top = reinterpret_cast<uint64_t*>(pool);
-  uint64_t* cand = top + kMaxK;
-  uint32_t* lh = reinterpret_cast<uint32_t*>(pool + 2 * kMaxK * 8);
-  uint16_t* segmap = reinterpret_cast<uint16_t*>(pool);
-  static_assert(sizeof(pool) >= 16384 * 2 && kMaxScanTiles <= 65536, "segment map");
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  constexpr int NWAVE = kSelThreads / 64;
-  constexpr int KPT = 16;  // keys per thread when the image's positive keys fit in registers
-  const int T = w.tiles;
-  const uint64_t* kb = w.keys + (size_t)b * T * kScanElems;
-  // segment counts -> exclusive prefix (tcnt[t] = first key of segment t), total n
-  {
-    uint32_t v[4], sum = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = 4 * tid + i;
-      v[i] = t < T ? w.cnt[(size_t)b * T + t] : 0u;
-      sum += v[i];
-    }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(incl, o);
-      if (lane >= o) incl += u;
-    }
-    if (lane == 63) sh.red_n[wave] = (int)incl;
-    if (tid == 0) { cnt_thr = 0; ncand = 0; }
-    __syncthreads();
-    uint32_t before = incl - sum + (uint32_t)wave_excl_prefix(sh.red_n, wave);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = 4 * tid + i;
-      if (t < T) tcnt[t] = before;
-      before += v[i];
-    }
-    if (tid == kSelThreads - 1) sh.nreal = (int)before;
-    __syncthreads();
-  }
-  const int n = sh.nreal;
-  // the keys in registers when they fit (key i = tid + j * NT), through a key -> segment map
-  const bool cached = n <= KPT * kSelThreads;
-  uint64_t rk[KPT];
-  if (cached) {
-    for (int t = wave; t < T; t += NWAVE) {
-      const int c0 = (int)tcnt[t];
-      const int c = (t + 1 < T ? (int)tcnt[t + 1] : n) - c0;
-      for (int i = lane; i < c; i += 64) segmap[c0 + i] = (uint16_t)t;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-      const int i = tid + j * kSelThreads;
-      const int t = i < n ? (int)segmap[i] : 0;
-      rk[j] = i < n ? kb[(size_t)t * kScanElems + (i - (int)tcnt[t])] : 0ull;
-    }
-    __syncthreads();  // the map is dead: lh / cand / top reuse its LDS
-  }
-  for (int i = tid; i < kHistBins; i += kSelThreads) lh[i] = 0;
+  if (last_flag != (uint32_t)(w.tiles - 1)) return;  // workgroup-uniform
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: every key load below is sc1
+  if (threadIdx.x == 0) seg_base = __hip_atomic_load((gu32*)(w.img_cnt + b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  // every positive key of the image (wave-uniform calls): registers, or the segments in global
-  // memory (wave w walking segments w, w + 16, ...) when the image has too many
-  auto for_each_key = [&](auto&& f) __attribute__((always_inline)) {
-    if (cached) {
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) f(rk[j], tid + j * kSelThreads < n);
-    } else {
-      for (int t = wave; t < T; t += NWAVE) {
-        const int c0 = (int)tcnt[t];
-        const int c = (t + 1 < T ? (int)tcnt[t + 1] : n) - c0;
-        const uint64_t* sk = kb + (size_t)t * kScanElems;
-        for (int i0 = 0; i0 < c; i0 += 64) {
-          const int i = i0 + lane;
-          const bool valid = i < c;
-          f(valid ? sk[i] : 0ull, valid);
-        }
-      }
-    }
-  };
-
-  if (n >= K) {
-    const int cap = K > kRankCap ? K : kRankCap;
-    // level 0: the 12 bits just below the bits every key shares (block min / max), so a map
-    // whose peak scores crowd into a narrow range still spreads over the bins
-    uint64_t lo = ~0ull, hi = 0;
-    {
-      int dummy = 0;
-      for_each_key([&](uint64_t key, bool valid) {
-        if (valid) {
-          lo = key < lo ? key : lo;
-          hi = key > hi ? key : hi;
-        }
-      });
-      block_minmax_sum<kSelThreads>(lo, hi, dummy, sh);
-    }
-    const uint64_t diff = lo ^ hi;
-    const int msb = diff ? 63 - __builtin_clzll(diff) : 0;
-    int shift = msb > kHistBits - 1 ? msb - (kHistBits - 1) : 0;
-    const uint64_t common = shift + kHistBits >= 64 ? 0ull : hi >> (shift + kHistBits);
-    for_each_key([&](uint64_t key, bool valid) { hist_add(lh, (uint32_t)(key >> shift) & (kHistBins - 1), valid); });
-    __syncthreads();
-    uint32_t c4[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c4[i] = lh[kHistBins - 1 - 4 * tid - i];
-    topdown_pick<kSelThreads>(c4, kHistBins, K, sh);
-    uint64_t prefix = (common << kHistBits) | (uint64_t)sh.sel_digit;
-    int above = sh.sel_above, bc = sh.sel_count;
-    __syncthreads();
-    // refine inside the threshold bucket until at most `cap` keys remain candidates
-    while (above + bc > cap && shift > 0) {
-      const int ns = shift > kHistBits ? shift - kHistBits : 0;
-      const int bits = shift - ns;
-      for (int i = tid; i < kHistBins; i += kSelThreads) lh[i] = 0;
-      __syncthreads();
-      for_each_key([&](uint64_t key, bool valid) {
-        hist_add(lh, (uint32_t)(key >> ns) & ((1u << bits) - 1), valid && (key >> shift) == prefix);
-      });
-      __syncthreads();
-      const int D = 1 << bits;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int d = D - 1 - 4 * tid - i;
-        c4[i] = d >= 0 ? lh[d] : 0u;
-      }
-      topdown_pick<kSelThreads>(c4, D, K - above, sh);
-      prefix = (prefix << bits) | (uint64_t)sh.sel_digit;
-      above += sh.sel_above;
-      bc = sh.sel_count;
-      shift = ns;
-      __syncthreads();
-    }
-    // candidates: every key whose top bits are >= the threshold digit path (above + bc of them)
-    if (cached) {
-      // wave counts -> wave offsets (one barrier), then ballot positions: no returning atomics
-      uint64_t bal[KPT];
-      int wc = 0;
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) {
-        bal[j] = __ballot(tid + j * kSelThreads < n && (rk[j] >> shift) >= prefix);
-        wc += (int)__popcll(bal[j]);
-      }
-      if (lane == 0) sh.red_n[wave] = wc;
-      __syncthreads();
-      int pos = wave_excl_prefix(sh.red_n, wave);
-      if (tid == kSelThreads - 1) ncand = pos + wc;
-      const uint64_t lt = (1ull << lane) - 1;
-#pragma unroll
-      for (int j = 0; j < KPT; ++j) {
-        if ((bal[j] >> lane) & 1ull) cand[pos + (int)__popcll(bal[j] & lt)] = rk[j];
-        pos += (int)__popcll(bal[j]);
-      }
-    } else {
-      for_each_key([&](uint64_t key, bool valid) {
-        const bool in = valid && (key >> shift) >= prefix;
-        const int slot = wave_append_slot(&ncand, in);
-        if (in) cand[slot] = key;
-      });
-    }
-    __syncthreads();
-    const int m = ncand;
-    if (m <= kSelThreads / 4) {
-      // four threads per candidate (adjacent lanes), each counting a quarter of the larger keys
-      const int ci = tid >> 2, part = tid & 3;
-      const uint64_t mykey = ci < m ? cand[ci] : 0;
-      int r = 0;
-#pragma unroll 8
-      for (int j = part; j < m; j += 4) r += cand[j] > mykey ? 1 : 0;
-      r += __shfl_xor(r, 1);
-      r += __shfl_xor(r, 2);
-      if (ci < m && part == 0 && r < K) top[r] = mykey;
-    } else if (tid < m) {
-      const uint64_t mykey = cand[tid];
-      int r = 0;
-#pragma unroll 8
-      for (int j = 0; j < m; ++j) r += cand[j] > mykey ? 1 : 0;
-      if (r < K) top[r] = mykey;
-    }
-    __syncthreads();
-  } else {
-    // fewer positive keys than K: exact streaming select over every key of the image
-    constexpr int PER = 16, CH = (PER - 1) * kSelThreads;
-    const float* base = heat + b * s0;
-    int have = 0;
-    for (uint32_t e0 = 0; e0 < w.N; e0 += CH) {
-      uint64_t k[PER];
-      int loc = 0;
-#pragma unroll
-      for (int j = 0; j < PER - 1; ++j) {
-        const uint32_t e = e0 + tid + j * kSelThreads;
-        k[j] = e < w.N ? nms_key_global(base, s1, s2, s3, H, W, e) : 0;
-        loc += k[j] != 0;
-      }
-      k[PER - 1] = tid < have ? top[tid] : 0;
-      loc += k[PER - 1] != 0;
-      const int real = block_count_real<kSelThreads>(loc, sh);
-      const int kt = min(K, real);
-      const uint64_t T2 = block_select<kSelThreads, PER>(k, kt, sh);
-      if (tid == 0) sh.nout = 0;
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < PER; ++j)
-        if (k[j] != 0 && k[j] >= T2) top[atomicAdd(&sh.nout, 1)] = k[j];
-      __syncthreads();
-      have = kt;
-    }
-    int P = 1;
-    while (P < K) P <<= 1;
-    for (int i = have + tid; i < P; i += kSelThreads) top[i] = 0;
-    __syncthreads();
-    bitonic_desc<kSelThreads>(top, P);
+  const int n = (int)seg_base;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store((gu32*)(w.img_cnt + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(w.ticket + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  write_outputs<kSelThreads>(top, K, b, mo, p, cnt_thr);
+  DSTAMP(stamps, 5);
+  fused_select<kScanThreads>(krs, n, b, heat, s0, s1, s2, s3, H, W, K, w.N, ssh, reinterpret_cast<char*>(tile), &ncand,
+                             &cnt_thr, mo, p, stamps);
 }
 
 // ---- host side --------------------------------------------------------------------------
@@ -1143,11 +1225,13 @@ TileGeom scan_geom(int C, int H, int W, int chan_fast) {
 }
 }  // namespace
 
+// [B] key counts + [B] tickets (zero between calls), then [B][tiles][kScanElems] keys
+size_t decode_head_bytes(int B) { return ((size_t)B * 8 + 255) / 256 * 256; }
 size_t decode_workspace_bytes(int B, int C, int H, int W, int K) {
   (void)K;
   const TileGeom g = scan_geom(C, H, W, 1);
   const size_t T = (size_t)g.ncg * g.nth * g.ntw;
-  return ((size_t)B * T * 4 + 255) / 256 * 256 + (size_t)B * T * kScanElems * 8;
+  return decode_head_bytes(B) + (size_t)B * T * kScanElems * 8;
 }
 
 int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, int W, int K, void* ws,
@@ -1160,12 +1244,17 @@ int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, i
   const TileGeom g = scan_geom(C, H, W, st[1] < st[3] ? 1 : 0);
   const int tiles = g.ncg * g.nth * g.ntw;
   if (tiles > kMaxScanTiles || B > 65535) { set_error("decode: heatmap too large (tiles per image)"); return 1; }
-  // the tile (+ halo) in fp32, later reused for the tile's compacted keys
-  const size_t lds = std::max((size_t)g.cg * (g.th + 2) * ((((g.tw + 2) + 3) & ~3) + 4) * sizeof(float),
-                              (size_t)kScanElems * sizeof(uint64_t));
+  // the tile (+ halo) in fp32, later reused for the tile's compacted keys (at most one per tile
+  // element) and the select's lists (top: K rounded up to a power of two; candidates)
+  int P = 1;
+  while (P < K) P <<= 1;
+  const size_t lds = std::max({(size_t)g.cg * (g.th + 2) * ((((g.tw + 2) + 3) & ~3) + 4) * sizeof(float),
+                               (size_t)g.cg * g.th * g.tw * sizeof(uint64_t),
+                               (size_t)(std::max(P, 2) + std::max(K, kRankCap) + 2) * sizeof(uint64_t)});
   ScanWs w;
-  w.cnt = (uint32_t*)ws;
-  w.keys = (uint64_t*)((char*)ws + ((size_t)B * tiles * 4 + 255) / 256 * 256);
+  w.img_cnt = (uint32_t*)ws;
+  w.ticket = w.img_cnt + B;
+  w.keys = (uint64_t*)((char*)ws + decode_head_bytes(B));
   w.tiles = tiles;
   w.N = (uint32_t)n;
   // per-image element offsets in 32 bits
@@ -1176,19 +1265,16 @@ int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, i
   }
   const bool vec4 = g.chan_fast && st[1] == 1 && C == 4 && g.cg == 4 && st[3] % 4 == 0 && st[2] % 4 == 0 &&
                     st[0] % 4 == 0 && ((uintptr_t)heat & 15) == 0;
+  const MergeOut mo{nullptr, nullptr, 1};
   if (vec4)
     hipLaunchKernelGGL(peak_scan<2>, dim3(tiles, B), dim3(kScanThreads), lds, s, heat, st[0], (int)st[1], (int)st[2],
-                       (int)st[3], C, H, W, K, g, w);
+                       (int)st[3], C, H, W, K, g, w, mo, rec);
   else if (g.chan_fast)
     hipLaunchKernelGGL(peak_scan<1>, dim3(tiles, B), dim3(kScanThreads), lds, s, heat, st[0], (int)st[1], (int)st[2],
-                       (int)st[3], C, H, W, K, g, w);
+                       (int)st[3], C, H, W, K, g, w, mo, rec);
   else
     hipLaunchKernelGGL(peak_scan<0>, dim3(tiles, B), dim3(kScanThreads), lds, s, heat, st[0], (int)st[1], (int)st[2],
-                       (int)st[3], C, H, W, K, g, w);
-  TV_HIP(hipGetLastError());
-  MergeOut mo{nullptr, nullptr, 1};
-  hipLaunchKernelGGL(peak_select, dim3(B), dim3(kSelThreads), 0, s, heat, st[0], st[1], st[2], st[3], H, W, K, w, mo,
-                     rec);
+                       (int)st[3], C, H, W, K, g, w, mo, rec);
   TV_HIP(hipGetLastError());
   return 0;
 }

@@ -109,9 +109,12 @@ class DeviceDecoder:
         need = ctypes.c_int64()
         _lib.check(_lib.lib().tv_decode_workspace_size(B, C, H, W, K, ctypes.byref(need)), "decode")
         self.ws_bytes = need.value
-        self.ws = torch.empty(need.value, dtype=torch.uint8, device=self.device)
-        self.records = torch.empty((B, K, REC), dtype=torch.float32, device=self.device)
-        self.counts = torch.empty((B,), dtype=torch.int32, device=self.device)
+        self.ws = torch.zeros(need.value, dtype=torch.uint8, device=self.device)  # counters zero-filled (tv_decode keeps them so)
+        # records and counts in one allocation (`packed`): a single D2H copy carries both
+        nrec = B * K * REC
+        self.packed = torch.empty((nrec + B) * 4, dtype=torch.uint8, device=self.device)
+        self.records = self.packed[:nrec * 4].view(torch.float32).view(B, K, REC)
+        self.counts = self.packed[nrec * 4:].view(torch.int32)
 
     def __call__(self, heat, size, offset, depth, mode, ratio, in_h, in_w, thr, aux=None):
         B, C, H, W, K = self.shape

@@ -235,3 +235,65 @@ def test_decode_nhwc_aligned_heads_match_nchw():
     r2, c2 = dec(logits.cuda(), size.cuda(), offset.cuda(), None, 0, 4, 240, 320, 0.2)
     np.testing.assert_array_equal(r1, r2.cpu().numpy())
     np.testing.assert_array_equal(c1, c2.cpu().numpy())
+
+
+@pytest.mark.parametrize("B,C,H,W,K,scale", [
+    (2, 4, 120, 160, 300, 3.0),     # K > 256: candidates over several threads each
+    (1, 4, 400, 400, 1024, 3.0),    # ~10^5 appended keys: the select streams them from global memory
+    (2, 2, 40, 50, 1000, 0.05),     # < K positive peaks per image with K > 256: streaming fallback carry
+    (3, 1, 7, 9, 20, 2.0),          # one tile per image: the scanning workgroup selects itself
+])
+def test_decode_single_launch_large_k_and_streaming(B, C, H, W, K, scale):
+    """tv_decode's single launch (the image's last scan workgroup selects) against the CPU oracle at
+    K beyond the direct-rank cap, an image whose kept keys exceed the register cache, images with
+    fewer positive peaks than K, and a one-tile image; called twice through one workspace (the
+    counters it leaves at zero)."""
+    from tauv_vision_amd.decode import DeviceDecoder
+    g = torch.Generator().manual_seed(B * 1000 + K)
+    logits = torch.randn((B, C, H, W), generator=g) * scale
+    if scale < 1.0:  # few positive peaks: a handful of raised cells on a saturated-to-zero map
+        logits.fill_(-200.0)
+        for b in range(B):
+            pos = torch.randperm(C * H * W, generator=g)[:40]
+            logits[b].view(-1)[pos] = torch.rand(40, generator=g) * 4.0
+    size = torch.randn((B, H, W, 2), generator=g)
+    offset = torch.rand((B, H, W, 2), generator=g)
+    dec = DeviceDecoder(B, C, H, W, K, torch.device("cuda"))
+    nms = oracle.heatmap_nms(torch.sigmoid(logits), 3).reshape(B, -1).numpy()
+    ref_s, ref_i = _tie_rule_topk(nms, K)
+    for _ in range(2):
+        rec, cnt = dec(logits.cuda(), size.cuda(), offset.cuda(), None, 0, 4, 4 * H, 4 * W, 0.0)
+        rec = rec.cpu().numpy()
+        np.testing.assert_array_equal(rec[..., 7].astype(np.int64), ref_i)
+        np.testing.assert_allclose(rec[..., 1], ref_s, rtol=0, atol=1e-6)
+        assert (cnt.cpu().numpy() == K).all()
+    assert int(dec.ws[:8 * B].view(torch.int32).abs().sum()) == 0, "counters not left at zero"
+
+
+def test_decode_graph_replay():
+    """DeviceDecoder captured in a HIP graph: replays on new heatmaps give the eager records (the
+    single launch resets its own counters; no memset node)."""
+    from tauv_vision_amd.decode import DeviceDecoder
+    B, C, H, W, K = 4, 4, 120, 160, 100
+    g = torch.Generator().manual_seed(3)
+    heat = (torch.randn((B, C, H, W), generator=g) * 2.0).cuda()
+    size = torch.randn((B, H, W, 2), generator=g).cuda()
+    offset = torch.rand((B, H, W, 2), generator=g).cuda()
+    dec = DeviceDecoder(B, C, H, W, K, torch.device("cuda"))
+    dec(heat, size, offset, None, 0, 4, 480, 640, 0.3)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            rec_g, cnt_g = dec(heat, size, offset, None, 0, 4, 480, 640, 0.3)
+    for seed in (10, 11, 12):
+        heat.copy_(torch.randn((B, C, H, W), generator=torch.Generator().manual_seed(seed)).cuda() * 2.0)
+        rec_g.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        got_r, got_c = rec_g.cpu().clone(), cnt_g.cpu().clone()
+        ref = DeviceDecoder(B, C, H, W, K, torch.device("cuda"))
+        r2, c2 = ref(heat, size, offset, None, 0, 4, 480, 640, 0.3)
+        assert torch.equal(got_c, c2.cpu())
+        assert torch.equal(got_r.nan_to_num(-7.0), r2.cpu().nan_to_num(-7.0))

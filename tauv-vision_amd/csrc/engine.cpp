@@ -317,6 +317,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_LAT") lat_mode = v;
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
+    else if (k == "TV_LAT_SPLIT_MIN") lat_split_min_nks = std::max(0, v);
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
     else if (k == "TV_CT3") ct3_mode = v ? 1 : 0;
     else if (k == "TV_BURST") burst_mode = std::max(0, std::min(2, v));
@@ -1043,7 +1044,11 @@ int Engine::make_workspace(int B, Workspace* ws) {
       if (!ws->lat[i]) continue;
       ConvParams& p = ws->params[i];
       const int tiles = p.mtiles * p.ntiles;
-      int ks = std::min(lat_split_max, p.nks / 2);
+      // only layers with a long k-step chain: measured at B=1 (profiles/r5/b1_knobs.txt), the hand-off
+      // (write-through partial tiles, ticket, sc1 loads) costs more than it saves on the 18-20 k-step
+      // 128-channel layers (R18 1.295 -> 1.269 ms without it) and far less on DLA-34's 36-72 k-step
+      // 256 / 512-channel ones (1.284 -> 1.398 ms without it)
+      int ks = p.nks >= lat_split_min_nks ? std::min(lat_split_max, p.nks / 2) : 1;
       ks = std::min(ks, cu_count / std::max(1, tiles));
       p.ksplit = ks > 1 ? ks : 0;
       if (!p.ksplit) continue;

@@ -100,6 +100,7 @@ struct Engine {
   int burst_mode = 1;          // conv_burst.hip for the small conv_lat layers it represents (knob TV_BURST=0 off,
                                // 2 = every layer it represents: diagnostics / tests)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)
+  int lat_split_min_nks = 32;  // ... for layers of at least this many k-steps (knob TV_LAT_SPLIT_MIN)
   int stamp_op = -1;           // diagnostics: op whose conv3x3 launch gets a stamp buffer (knob TV_C3_STAMPS=op:ptr)
   unsigned long long* stamp_buf = nullptr;
   int profiled_u8 = 0;         // input kind of the last profile() (kernel instance names)

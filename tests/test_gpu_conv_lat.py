@@ -76,14 +76,15 @@ def test_lat_default_selection_b32():
 
 
 def test_lat_split_k_b1(monkeypatch):
-    """At B=1 the conv_lat layers run split-K over workgroups (several workgroups per tile, the
-    last to arrive sums the fp32 partial tiles in slice order): repeated forwards are bit-identical
-    whichever workgroup arrives last, and the result matches the unsplit kernel (knob
-    TV_LAT_SPLIT=1) within the fp16 tolerance of the golden comparison."""
+    """At B=1 the conv_lat layers can run split-K over workgroups (several workgroups per tile, the
+    last to arrive sums the fp32 partial tiles in slice order; by default only layers of >= 32
+    k-steps, so here forced for R18's 18-20 k-step layers with TV_LAT_SPLIT_MIN=0): repeated forwards
+    are bit-identical whichever workgroup arrives last, and the result matches the unsplit kernel
+    (knob TV_LAT_SPLIT=1) within the fp16 tolerance of the golden comparison."""
     from tauv_vision_amd import engine as E
     name = "r18_c128_b1_480x640"
     img = case_input(name).cuda()
-    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_BURST": "0"})  # every deep layer on conv_lat
+    monkeypatch.setattr(E, "_DIAG_KNOBS", {"TV_BURST": "0", "TV_LAT_SPLIT_MIN": "0"})  # every deep layer on conv_lat, split
     model, oc, mc, case = fwd.build(name, "fp16")
     runs = [model(img) for _ in range(3)]
     for f in ("heatmap", "size", "offset"):

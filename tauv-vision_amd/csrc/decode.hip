@@ -582,16 +582,6 @@ __device__ __forceinline__ int wave_append_slot(int* counter, bool pred) {
   return base + (int)__popcll(bal & ((1ull << lane) - 1));
 }
 
-// Sum of arr[0 .. wave) (per-wave totals published in LDS), read lane-parallel and reduced with
-// cross-lane adds instead of a dependent chain of LDS reads.
-__device__ __forceinline__ int wave_excl_prefix(const int* arr, int wave) {
-  const int lane = threadIdx.x & 63;
-  int v = lane < wave ? arr[lane] : 0;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
-
 // LDS histogram increment that stays cheap whether the wave's bins crowd or spread: the lanes
 // sharing the first active lane's bin add once (one atomic), the others add individually.
 // Call from wave-uniform control flow.
@@ -778,14 +768,12 @@ __device__ void fused_select(const i32x4 krs, int n, int b, const float* __restr
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // (the pad key)
       int r = 0;
       const int m2 = (m + 1) >> 1;
-      typedef const __attribute__((address_space(3))) ulonglong2 lds_u2;
       const ulonglong2* c2 = reinterpret_cast<const ulonglong2*>(cand);
 #pragma unroll 8
       for (int j = 0; j < m2; ++j) {
         const ulonglong2 v = c2[j];
         r += (v.x > mykey ? 1 : 0) + (v.y > mykey ? 1 : 0);
       }
-      (void)sizeof(lds_u2);
       if (tid < m && r < K) local_thr += store_record(mykey, in, r, K, b, mo, p);
     } else {
       for (int ci = tid; ci < m; ci += NT) {

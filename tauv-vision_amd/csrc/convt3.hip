@@ -9,18 +9,21 @@
 // 3x3 conv's reuse, but the round-4 engine ran them as 4 separate implicit GEMMs (conv_pipe: the
 // input read once per phase, 1-4 taps of K per launch: ~430 TFLOP/s).
 //
-// Here a workgroup (8 waves, one per CU, persistent over a static unit list) owns a 16 x 16 tile of
-// input pixels x 64 output channels x all 4 phases: wave w owns input rows 2w, 2w + 1 (two 16-pixel
-// fragments) x 64 channels x 4 phases = 32 accumulators of v_mfma_f32_16x16x32 (128 VGPRs).
-// K order: channel blocks of 32; per block the (16 + 1) x (16 + 1) input halo moves into LDS once
-// (LDS-DMA, 80-byte pixel pitch, out-of-image pixels and the pad slot buffer-OOB zeros) together
-// with the block's 9 (phase, tap) weight fragments x 64 channels (36 KiB, pre-packed in MFMA
-// A-operand lane order: one contiguous 1 KiB LDS-DMA piece per fragment); the next block (or the
-// next unit's first) streams into the other buffers under the current block's 72 MFMAs per wave;
-// one barrier per block. The input fragments use conv3x3.hip's conflict-free lane permutation
-// (pixel pi(n), 16-byte chunk sigma(c)); the weights carry the matching channel order. Epilogue
-// from the accumulators: bias, activation, one rounding, v_permlane16_swap into 16-byte stores of
-// each phase's output pixels (2m + pi, 2n + pj).
+// Here a workgroup (8 waves, one per CU, persistent over a static, XCD-contiguous unit list) owns a
+// tile of tw x tr <= 256 input pixels (shape chosen per layer: convt3_tile) x 64 output channels x
+// all 4 phases: wave w owns tile pixels 32 w .. 32 w + 31 in raster order (two 16-pixel fragments,
+// which may span tile rows) x 64 channels x 4 phases = 32 accumulators of v_mfma_f32_16x16x32
+// (128 VGPRs). K order: channel blocks of 32; per block the (tw + 1) x (tr + 1) input halo moves
+// into LDS once (LDS-DMA, 80-byte pixel pitch, out-of-image pixels and the pad slot buffer-OOB
+// zeros) together with the block's 9 (phase, tap) weight fragments x 64 channels (36 KiB, pre-packed
+// in MFMA A-operand lane order: one contiguous 1 KiB LDS-DMA piece per fragment) and, with a unit's
+// last block, its biases; the next block (or the next unit's first) streams into the other buffer
+// set under the current block's 72 MFMAs per wave, whose weight fragments come through a ring of
+// registers CT3_WD fragments ahead. One raw barrier per block (counted vmcnt: a unit's epilogue
+// stores stay in flight across it). The input fragments use conv3x3.hip's conflict-free lane
+// permutation (pixel pi(n), 16-byte chunk sigma(c)); the weights carry the matching channel order.
+// Epilogue from the accumulators: bias, activation, one rounding, v_permlane16_swap into 16-byte
+// stores of each phase's output pixels (2m + pi, 2n + pj).
 #include "conv_common.h"
 
 #include <algorithm>

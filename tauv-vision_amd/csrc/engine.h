@@ -81,7 +81,8 @@ struct Engine {
                                // at B=1 the halo kernel beats the implicit GEMM on the small levels too)
   int c3_ni_force = 0;         // conv3x3 channel tile: 0 = by grid rounds, 2 / 4 forced (env TV_C3_NI)
   int c3_nw_mode = 0;          // conv3x3 workgroup size: 0 = 4-wave where eligible, 8 = always 8 (TV_C3_NW)
-  int c3_half_cost = 55;       // cost of a 64-channel half tile in % of a full one (env TV_C3_HALF_COST, 0 = never)
+  int c3_half_cost = 70;       // cost of a 64-channel half tile in % of a full one (env TV_C3_HALF_COST, 0 = never;
+                               // swept r5: 70-85 best at B=64, 100 loses B=1, profiles/r5/half_cost_sweep.txt)
   int conv3_min_pix = 1;       // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)
   int s2_mode = 1;             // stride-2 halo kernel for eligible fp16/bf16 layers (env TV_CONV3S2=0 off)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)

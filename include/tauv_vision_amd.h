@@ -271,6 +271,17 @@ int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg
                        const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, void* out,
                        int32_t out_ldc, void* stream);
 
+/* Diagnostics (GPU tests): one narrow-channel Conv2d(C, N, 3, stride, padding 1) + bias + activation
+ * (DLA-34's full-resolution base levels, centerpoint_dla.py:242-246 `_make_conv_level`) through
+ * conv_small, the engine's kernel for them: C -> N in {16 -> 16, 16 -> 32, 32 -> 32 (stride 1),
+ * 32 -> 64 (stride 2)}. src: compute-dtype NHWC [B, H, W, ldc]; weight: host fp32 [N][C][3][3];
+ * bias: host fp32 [N]; out: compute-dtype NHWC [B, Ho, Wo, out_ldc]. variant: 0 = per-lane register
+ * gathers, 1 = LDS-halo tiles (a tile per workgroup), 2 = LDS-halo tiles on a persistent grid. TV_F16 / TV_BF16; TV_EINVAL for shapes the kernel does not take.
+ * Synchronous; allocates. */
+int tv_diag_conv_small(const void* src, int32_t B, int32_t H, int32_t W, int32_t C, int32_t ldc, const float* weight,
+                       const float* bias, int32_t N, int32_t stride, int32_t act, int32_t dtype, int32_t variant,
+                       void* out, int32_t out_ldc, void* stream);
+
 /* Diagnostics (GPU tests): one ConvTranspose2d(C, N, 3, stride 2, padding 1, output_padding 1) +
  * bias + activation (YOLACT protonet up-sampling, masknet.py:21,33) through convt3, the engine's
  * kernel for it. src: compute-dtype NHWC [B, H, W, ldc], C channels (a multiple of 32); weight: host

@@ -387,6 +387,13 @@ int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg
                                         (hipStream_t)stream); })
 }
 
+int tv_diag_conv_small(const void* src, int32_t B, int32_t H, int32_t W, int32_t C, int32_t ldc, const float* weight,
+                       const float* bias, int32_t N, int32_t stride, int32_t act, int32_t dtype, int32_t variant,
+                       void* out, int32_t out_ldc, void* stream) {
+  TV_GUARD({ return tv::diag_conv_small(src, B, H, W, C, ldc, weight, bias, N, stride, act, dtype, variant, out,
+                                        out_ldc, (hipStream_t)stream); })
+}
+
 int tv_diag_convt3(const void* src, int32_t B, int32_t H, int32_t W, int32_t C, int32_t ldc, const float* weight,
                    const float* bias, int32_t N, int32_t act, int32_t dtype, int32_t tile_w, int32_t tile_h, void* out,
                    int32_t out_ldc, void* stream) {

@@ -222,6 +222,9 @@ int diag_conv1x1(const void* const* src, const int* C, const int* ldc, int nseg,
 int diag_conv_burst(const void* const* src, const int* geom, int nseg, int B, int Ho, int Wo, const float* weight,
                     const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s);
 
+// diag.cpp: one narrow-channel 3x3 conv through conv_small (GPU tests)
+int diag_conv_small(const void* src, int B, int H, int W, int C, int ldc, const float* weight, const float* bias,
+                    int N, int stride, int act, int dtype, int halo, void* out, int out_ldc, hipStream_t s);
 // diag.cpp: one ConvTranspose2d(3, s2, p1, op1) + bias + activation through convt3 (GPU tests)
 int diag_convt3(const void* src, int B, int H, int W, int C, int ldc, const float* weight, const float* bias, int N,
                 int act, int dtype, int tw, int tr, void* out, int out_ldc, hipStream_t s);
@@ -229,7 +232,9 @@ int diag_convt3(const void* src, int B, int H, int W, int C, int ldc, const floa
 // Narrow-channel 3x3 / pad 1 conv (conv_small.hip), fp16/bf16: 16 -> 16/32 and 32 -> 32/64 input ->
 // output channels at stride 1 or 2 (DLA-34 base levels), bias + activation, NHWC
 bool conv_small_supported(int cin, int cout, int stride, int cin_ldc, int out_ldc);
-int launch_conv_small(const ConvParams& p, const ConvParams* dp, int dtype, int cu_count, hipStream_t s);
+// halo: 0 = per-lane register gathers, 1 = LDS-halo tiles (input tile staged once by LDS-DMA), one
+// tile per workgroup, 2 = LDS-halo tiles on a persistent grid
+int launch_conv_small(const ConvParams& p, const ConvParams* dp, int dtype, int cu_count, int halo, hipStream_t s);
 
 // Fused input staging + 7x7 stem conv (stem.hip), fp16/bf16, C0 <= 128 output channels.
 struct StemParams {

@@ -317,4 +317,49 @@ int diag_convt3(const void* src, int B, int H, int W, int C, int ldc, const floa
   return TV_OK;
 }
 
+// One narrow-channel 3x3 pad-1 conv + bias + activation through conv_small.hip (the engine's kernel
+// for DLA-34's full-resolution base levels, centerpoint_dla.py:242-246): weight host fp32
+// [N][C][3][3] packed as the engine packs it ([N][Kpad], K tap-major, channel-minor); halo selects
+// the LDS-halo variant.
+int diag_conv_small(const void* src, int B, int H, int W, int C, int ldc, const float* weight, const float* bias,
+                    int N, int stride, int act, int dtype, int halo, void* out, int out_ldc, hipStream_t s) {
+  if (!src || !weight || !bias || !out || B < 1 || H < 1 || W < 1 || act < 0 || act > 2 || (stride != 1 && stride != 2) ||
+      (dtype != F16 && dtype != BF16) || !conv_small_supported(C, N, stride, ldc, out_ldc) || out_ldc < N) {
+    set_error("diag_conv_small: bad argument or shape not supported by conv_small");
+    return TV_EINVAL;
+  }
+  const int Kpad = (9 * C + 63) / 64 * 64;
+  std::vector<uint8_t> hw((size_t)N * Kpad * 2, 0);
+  for (int n = 0; n < N; ++n)
+    for (int c = 0; c < C; ++c)
+      for (int t = 0; t < 9; ++t) put(hw, (size_t)n * Kpad + t * C + c, weight[((size_t)n * C + c) * 9 + t], dtype);
+  ConvParams p{};
+  p.seg[0] = ConvSegment{src, H, W, C, ldc, 3, 3, stride, 1, 1, Kpad / 64, 0};
+  p.nseg = 1;
+  p.Ho = (H - 1) / stride + 1;
+  p.Wo = (W - 1) / stride + 1;
+  p.M = B * p.Ho * p.Wo;
+  p.N = N;
+  p.Kpad = Kpad;
+  p.act = act;
+  p.out = out;
+  p.out_ldc = out_ldc;
+  DevBuf dw, db, dp;
+  TV_HIP(hipMalloc(&dw.p, hw.size()));
+  TV_HIP(hipMemcpy(dw.p, hw.data(), hw.size(), hipMemcpyHostToDevice));
+  TV_HIP(hipMalloc(&db.p, (size_t)N * 4));
+  TV_HIP(hipMemcpy(db.p, bias, (size_t)N * 4, hipMemcpyHostToDevice));
+  p.weight = dw.p;
+  p.bias = (const float*)db.p;
+  TV_HIP(hipMalloc(&dp.p, sizeof(ConvParams)));
+  TV_HIP(hipMemcpy(dp.p, &p, sizeof(ConvParams), hipMemcpyHostToDevice));
+  int dev = 0, ncu = 256;
+  TV_HIP(hipGetDevice(&dev));
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu < 1) ncu = 256;
+  const int rc = launch_conv_small(p, (const ConvParams*)dp.p, dtype, ncu, halo, s);
+  if (rc) return rc == TV_EHIP ? rc : TV_EINVAL;
+  TV_HIP(hipStreamSynchronize(s));
+  return TV_OK;
+}
+
 }  // namespace tv

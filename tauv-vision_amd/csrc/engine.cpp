@@ -332,6 +332,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_C3_NI") c3_ni_force = v == 2 ? 2 : v == 4 ? 4 : 0;
     else if (k == "TV_C3_NW") c3_nw_mode = v == 8 ? 8 : 0;
     else if (k == "TV_C3_HALF_COST") c3_half_cost = v;
+    else if (k == "TV_CSM_HALO") csm_halo = std::max(0, std::min(2, v));
     else if (k == "TV_SLICES") slices = std::max(1, std::min(kMaxSlices, v));
     else if (k == "TV_SLICE_LAG") slice_lag = std::max(0, v);
     else if (k == "TV_C3_STAMPS") {  // "op:device pointer" (stamp builds of conv3x3 only)
@@ -1268,7 +1269,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   if (op.out < 0) p.out = out;
   const bool out_f32 = op.out < 0;
   const int mode = op.kind == OP_CONVT_ADD || op.up_s ? 1 : 0;
-  if (ws->small[i]) return launch_conv_small(p, ws->dparams + i, dtype, cu_count, s);
+  if (ws->small[i]) return launch_conv_small(p, ws->dparams + i, dtype, cu_count, csm_variant(p.seg[0].stride), s);
   if (ws->burst[i]) {
     const BurstParams* bp = &ws->bparams[i];
     return launch_conv_burst(&bp, 1, dtype, s);
@@ -1474,7 +1475,7 @@ const char* Engine::op_kernel(int B, size_t i) {
         }
       }
       else if (ws->small[i])
-        name = std::string("tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
+        name = std::string(csm_variant(op.segs[0].stride) ? "tv::csm::conv_small_halo<" : "tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";
       else if (ws->lat[i])
         name = std::string("tv::lat::conv_lat<") + t + ">";

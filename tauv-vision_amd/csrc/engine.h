@@ -83,6 +83,10 @@ struct Engine {
   int c3_nw_mode = 0;          // conv3x3 workgroup size: 0 = 4-wave where eligible, 8 = always 8 (TV_C3_NW)
   int c3_half_cost = 70;       // cost of a 64-channel half tile in % of a full one (env TV_C3_HALF_COST, 0 = never;
                                // swept r5: 70-85 best at B=64, 100 loses B=1, profiles/r5/half_cost_sweep.txt)
+  int csm_halo = 2;            // conv_small.hip variant (knob TV_CSM_HALO): 0 = register gathers, 1 = LDS-halo
+                               // tiles, one per workgroup, 2 = LDS-halo tiles on a persistent grid (measured r5:
+                               // fastest for all three DLA-34 layers, profiles/r5/csm_halo.txt)
+  int csm_variant(int stride) const { return stride > 0 ? csm_halo : 0; }
   int conv3_min_pix = 1;       // halo kernels only for frames of >= this many pixels (env TV_CONV3_MINPIX)
   int s2_mode = 1;             // stride-2 halo kernel for eligible fp16/bf16 layers (env TV_CONV3S2=0 off)
   int conv3_mode = 1;          // persistent halo 3x3 kernel for eligible fp16/bf16 layers (env TV_CONV3=0 off)

@@ -73,6 +73,8 @@ EXPORTS = {
                                    c_f64, c_f64, c_vp, c_vp, c_vp, c_vp], c_i32),
     "tv_diag_dcn_conv": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32,
                           c_vp, c_vp], c_i32),
+    "tv_diag_conv_small": ([c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32,
+                            c_vp, c_i32, c_vp], c_i32),
     "tv_diag_convt3": ([c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
                         c_i32, c_vp], c_i32),
     "tv_diag_conv1x1": ([c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp], c_i32),

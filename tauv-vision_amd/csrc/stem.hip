@@ -33,13 +33,23 @@ constexpr int EPIX = 48;                     // bytes per expanded pixel (24 val
 constexpr int EBUF = RR * TW * EPIX;         // 33,792
 constexpr int KS = 11;                       // MFMA k-steps (K = 176 >= 168)
 constexpr int WF_BYTES = KS * 4 * 64 * 16;   // weights in B-fragment order = 45,056
-constexpr int OFF_E = 0;
-constexpr int OFF_W = OFF_E + 2 * EBUF;
-constexpr int OFF_N = OFF_W + WF_BYTES;
-constexpr int OFF_LUT = OFF_N + RR * NPITCH;
-constexpr int OFF_B = OFF_LUT + 768 * 2;
-constexpr int LDS = OFF_B + 128 * 4;
-static_assert(LDS <= 160 * 1024, "LDS budget");
+// LDS layout per NI. NI = 4: two E buffers (the next tile expanded while this one's MFMAs run),
+// one 512-thread workgroup per CU. NI = 1 (16-32 output channels: little MFMA work per tile, the
+// window staging and expansion dominate): one E buffer and only the 11 KiB of block-0 weight
+// fragments, 53 KiB in all, so several workgroups per CU overlap one's staging with another's
+// MFMAs (round 5: the workgroup's own double buffering left the staging serial).
+template <int NI> struct Lay {
+  static constexpr int NE = NI == 1 ? 1 : 2;
+  static constexpr int OFF_E = 0;
+  static constexpr int OFF_W = OFF_E + NE * EBUF;
+  static constexpr int WBYTES = KS * NI * 64 * 16;   // fragments (k-step j, block i) at (j NI + i) KiB
+  static constexpr int OFF_N = OFF_W + WBYTES;
+  static constexpr int OFF_LUT = OFF_N + RR * NPITCH;
+  static constexpr int OFF_B = OFF_LUT + 768 * 2;
+  static constexpr int LDS = OFF_B + 128 * 4;
+  static constexpr int WGS = NI == 1 ? 2 : 1;        // workgroups per CU the grid is sized for (3 spills)
+  static_assert(LDS * WGS <= 160 * 1024, "LDS budget");
+};
 
 __constant__ float kMean[3] = {0.485f, 0.456f, 0.406f};
 __constant__ float kStd[3] = {0.229f, 0.224f, 0.225f};
@@ -69,8 +79,10 @@ template <> struct Window<2> { static constexpr int NS = (RR * 30 + NT - 1) / NT
 // NI: 32-channel output blocks computed (4 for C0 = 128; 1 for DLA-34's 16-channel base layer,
 // whose tiles would otherwise spend 3/4 of their MFMAs and epilogue on padding channels)
 template <typename T, int MODE, int NI>
-__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2, 2))) void stem_conv(
-    StemParams p) {
+__global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_eu(2 * Lay<NI>::WGS, 2 * Lay<NI>::WGS)))
+void stem_conv(StemParams p) {
+  using L = Lay<NI>;
+  constexpr int OFF_E = L::OFF_E, OFF_W = L::OFF_W, OFF_N = L::OFF_N, OFF_LUT = L::OFF_LUT, OFF_B = L::OFF_B;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool U8 = MODE != 0;
   constexpr int NS = Window<MODE>::NS;
@@ -90,13 +102,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     const uint4* ws = reinterpret_cast<const uint4*>(p.weight);
     uint4* wd = reinterpret_cast<uint4*>(smem + OFF_W);
     // all loads issued before the LDS writes (one memory latency, not one per chunk)
-    constexpr int NCH = (WF_BYTES / 16 + NT - 1) / NT;
+    // LDS chunk d = fragment (j, i) = (d / 64 / NI, d / 64 % NI), 16-byte lane chunk d % 64, of the
+    // host's 4-block fragment order
+    constexpr int NCH = (L::WBYTES / 16 + NT - 1) / NT;
+    auto src_chunk = [](int d) { return ((d >> 6) / NI * 4 + (d >> 6) % NI) * 64 + (d & 63); };
     uint4 wv[NCH];
 #pragma unroll
-    for (int k = 0; k < NCH; ++k) wv[k] = tid + k * NT < WF_BYTES / 16 ? ws[tid + k * NT] : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < NCH; ++k)
+      wv[k] = tid + k * NT < L::WBYTES / 16 ? ws[src_chunk(tid + k * NT)] : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
-      if (tid + k * NT < WF_BYTES / 16) wd[tid + k * NT] = wv[k];
+      if (tid + k * NT < L::WBYTES / 16) wd[tid + k * NT] = wv[k];
     float* lb = reinterpret_cast<float*>(smem + OFF_B);
     if (tid < 128) lb[tid] = tid < p.N ? p.bias[tid] : 0.0f;
     if constexpr (U8) {
@@ -230,7 +246,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
       uint4 b[NI];
       const uint4 a = *reinterpret_cast<const uint4*>(base + off0 + f * TW * EPIX);
 #pragma unroll
-      for (int i = 0; i < NI; ++i) b[i] = *reinterpret_cast<const uint4*>(wfl + (j * 4 + i) * 1024);
+      for (int i = 0; i < NI; ++i) b[i] = *reinterpret_cast<const uint4*>(wfl + (j * NI + i) * 1024);
 #pragma unroll
       for (int i = 0; i < NI; ++i) Mfma<T>::run(b[i], a, acc[f][i]);
     }
@@ -282,6 +298,7 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
   // tile k of this block: t = t0 + k*G, E buffer k % 2, window of tile k+1 in set (k+1) % 2
   auto tile = [&](int t, int eb, unsigned (&raw_next)[NS], unsigned (&raw_k2)[NS]) __attribute__((always_inline)) {
     const int tn = t + G, tn2 = t + 2 * G;
+    if constexpr (L::NE == 1) eb = 0;
     if (tn2 < ntot) load_window(tn2, raw_k2);  // tile k's set: already consumed
     mfma_row(eb, std::integral_constant<int, 0>{});
     epilogue(t, std::integral_constant<int, 0>{});
@@ -289,8 +306,8 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
     epilogue(t, std::integral_constant<int, 1>{});
     if (tn < ntot) {
       store_window(tn, raw_next);  // N is free: its last reader (expand) finished before the last barrier
-      lds_barrier();
-      expand(eb ^ 1);  // E[eb ^ 1] was last read by the previous tile's MFMAs
+      lds_barrier();               // (one E buffer: also every wave's MFMA reads of E done)
+      expand(L::NE == 1 ? 0 : eb ^ 1);  // E[eb ^ 1] was last read by the previous tile's MFMAs
       lds_barrier();
     }
   };
@@ -303,15 +320,17 @@ __global__ __attribute__((amdgpu_flat_work_group_size(NT, NT), amdgpu_waves_per_
 template <typename T, int MODE, int NI>
 static int launch_t(const StemParams& p, int grid, hipStream_t s) {
   auto k = stem_conv<T, MODE, NI>;
-  if (int r = ensure_lds<stem_conv<T, MODE, NI>>(LDS)) return r;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), LDS, s, p);
+  if (int r = ensure_lds<stem_conv<T, MODE, NI>>(Lay<NI>::LDS)) return r;
+  const long ntot = (long)p.B * ((p.H + TH - 1) / TH) * ((p.W + TW - 1) / TW);
+  grid = (int)std::min<long>(ntot, (long)grid * Lay<NI>::WGS);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), Lay<NI>::LDS, s, p);
   TV_HIP(hipGetLastError());
   return 0;
 }
 
 }  // namespace stem
 
-size_t stem_weight_bytes() { return stem::WF_BYTES; }
+size_t stem_weight_bytes() { return stem::WF_BYTES; }  // the host's 4-block fragment order
 
 // [Npad][Kpad] packed stem weights (K = ky * 24 + kx * 3 + c) -> B-fragment order:
 // fragment (k-step j, channel block i), lane l: 8 values n = 32i + l%32, k = 16j + 8(l/32) + e

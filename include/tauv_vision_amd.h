@@ -163,7 +163,10 @@ int tv_index_split(const int32_t* flat, int32_t B, int32_t K, int32_t H, int32_t
  * aux_strides[5] (the [B,K,2,H,W] keypoint_affinity view).
  * workspace: tv_decode_workspace_size() bytes of device memory, ZERO-FILLED before its first use
  * (it carries the per-image peak keys and the arrival counters of the call's single launch, which
- * leaves the counters at zero again for the next call) — one call at a time per workspace. */
+ * leaves the counters at zero again for the next call) — one call at a time per workspace. The
+ * counters sit at fixed offsets (a 512 KiB head: one pair per image index up to 65535), so one
+ * zero-filled workspace serves every later call whose tv_decode_workspace_size() it covers, at
+ * any B or heatmap geometry. */
 int tv_decode_workspace_size(int32_t B, int32_t C, int32_t H, int32_t W, int32_t K, int64_t* bytes);
 int tv_decode(const float* heat, const int64_t heat_strides[4], const float* size, const int64_t size_strides[4],
               const float* offset, const int64_t offset_strides[4], const float* depth,
@@ -270,6 +273,13 @@ int tv_diag_conv1x1(const void* const* src, const int32_t* C, const int32_t* ldc
 int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg, int32_t B, int32_t Ho, int32_t Wo,
                        const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, void* out,
                        int32_t out_ldc, void* stream);
+
+/* Diagnostics (host only, no GPU needed): conv_burst's launch plan for a layer geometry (geom as
+ * tv_diag_conv_burst, N output channels). out[0] = 1 when the kernel takes the layer, out[1] its
+ * dynamic LDS bytes, out[2] the end of the highest LDS byte any of its accesses touches over every
+ * tile position (the kernel's own index arithmetic; <= out[1], else the plan refuses the layer),
+ * out[3] the LDS the layer's staging would need. */
+int tv_diag_burst_plan(const int32_t* geom, int32_t nseg, int32_t B, int32_t Ho, int32_t Wo, int32_t N, int32_t* out);
 
 /* Diagnostics (GPU tests): one narrow-channel Conv2d(C, N, 3, stride, padding 1) + bias + activation
  * (DLA-34's full-resolution base levels, centerpoint_dla.py:242-246 `_make_conv_level`) through

@@ -387,6 +387,10 @@ int tv_diag_conv_burst(const void* const* src, const int32_t* geom, int32_t nseg
                                         (hipStream_t)stream); })
 }
 
+int tv_diag_burst_plan(const int32_t* geom, int32_t nseg, int32_t B, int32_t Ho, int32_t Wo, int32_t N, int32_t* out) {
+  TV_GUARD({ return tv::diag_burst_plan(geom, nseg, B, Ho, Wo, N, out); })
+}
+
 int tv_diag_conv_small(const void* src, int32_t B, int32_t H, int32_t W, int32_t C, int32_t ldc, const float* weight,
                        const float* bias, int32_t N, int32_t stride, int32_t act, int32_t dtype, int32_t variant,
                        void* out, int32_t out_ldc, void* stream) {

@@ -1,6 +1,13 @@
 // Shared definitions for the tauv-vision_amd HIP library (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+// gfx950 only. The cross-workgroup hand-offs (decode.hip's single-launch select, conv_lat's split-K
+// tickets) rely on gfx950's SC1 cache-bit semantics: write-through sc1 stores and L1-bypassing sc1
+// loads stand in for a release / acquire pair (MI355X_MICROARCH.md, inter-workgroup visibility).
+// On another target they would compile cleanly and could read stale bytes through the L2.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "tauv_vision_amd kernels are written for gfx950 (MI355X) only"
+#endif
 #include <cstdint>
 #include <string>
 
@@ -135,6 +142,7 @@ struct BurstParams {
   void* out;
   int out_ldc, out_coff, N;
   int lds, zero_off;    // dynamic LDS bytes; the zero block's offset
+  int lds_end;          // conv_burst_lds_extent(): end of the highest LDS byte any access touches (<= lds)
 };
 struct BurstGroup {
   BurstParams p[kBurstGroupMax];
@@ -144,6 +152,7 @@ struct BurstGroup {
 // the launch geometry of a conv (p: the engine's ConvParams for a B-frame workspace); false when
 // the layer is not representable (strided 3x3, channel counts, LDS)
 bool conv_burst_plan(const ConvParams& p, int B, BurstParams* out);
+int conv_burst_lds_extent(const BurstParams& p);
 size_t conv_burst_weight_bytes(const BurstParams& p);
 int conv_burst_repack(const void* w, int Kpad, int esz, const BurstParams& p, void* out, hipStream_t s);
 int conv_burst_workgroups(const BurstParams& p);
@@ -219,6 +228,7 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
 int diag_conv1x1(const void* const* src, const int* C, const int* ldc, int nseg, int M, const float* weight,
                  const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s);
 // diag.cpp: one multi-segment conv (3x3 / 1x1 segments) through conv_burst (GPU tests)
+int diag_burst_plan(const int* geom, int nseg, int B, int Ho, int Wo, int N, int* out);
 int diag_conv_burst(const void* const* src, const int* geom, int nseg, int B, int Ho, int Wo, const float* weight,
                     const float* bias, int N, int act, int dtype, void* out, int out_ldc, hipStream_t s);
 
@@ -383,8 +393,10 @@ size_t select_workspace_bytes(int B, int C, int H, int W, int K);
 int launch_select(const float* heat, const int64_t st[4], int B, int C, int H, int W, int nms, int apply_sigmoid,
                   int K, void* ws, size_t ws_bytes, float* score, int32_t* index, const DecodeParams* rec,
                   hipStream_t s);
-// tv_decode's path (sigmoid + 3x3 NMS + exact top-K + records): peak_scan + peak_select
-// (decode.hip), workspace decode_workspace_bytes() (no initial contents needed).
+// tv_decode's path (sigmoid + 3x3 NMS + exact top-K + records): peak_scan, one launch (decode.hip).
+// Workspace: decode_workspace_bytes(), zero-filled once before its first use; its per-image
+// counters sit at fixed offsets (independent of B and of the heatmap geometry) and every call
+// leaves them at zero, so the zero-filled workspace serves any later call that fits it.
 size_t decode_workspace_bytes(int B, int C, int H, int W, int K);
 int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, int W, int K, void* ws,
                   size_t ws_bytes, const DecodeParams& rec, hipStream_t s);

@@ -266,6 +266,55 @@ static int burst_kpw(int nk16) {
   return 0;
 }
 
+// The exclusive end of every LDS byte burst_tile() touches for layer p, over every tile position of a
+// frame (the kernel's own index arithmetic, restated next to it so the two cannot drift apart), or -1
+// when a tap would read a window pixel the staging did not write (the read stays inside the LDS but
+// returns another segment's / plane's bytes). Round 5: B = 2, 15x20, one 128-channel 3x3 segment
+// faulted ("an illegal memory access", then NaN outputs once the fault was masked) while the kernel
+// was being written; an LDS address past the launch's dynamic allocation faults on gfx950.
+// conv_burst_plan() refuses a layer whose extent exceeds p.lds, and every launch re-checks it.
+int conv_burst_lds_extent(const BurstParams& p) {
+  using namespace burst;
+  const int hw = p.Ho * p.Wo;
+  int end = p.zero_off + ZERO_BYTES;                  // the zero block (written by 16 threads)
+  end = std::max(end, NW * PART);                     // the partial tiles (alias the staging)
+  for (int s = 0; s < p.nseg; ++s) {
+    const BurstSeg& sg = p.seg[s];
+    const int per_plane = sg.npix * SLOTS;
+    const int chunks = sg.planes * per_plane;
+    const int pieces = (chunks + 63) / 64;            // staging: piece q covers [q KiB, q KiB + 1 KiB)
+    if (s + 1 < p.nseg && sg.lds_off + pieces * 1024 > p.seg[s + 1].lds_off) return -1;
+    if (s + 1 == p.nseg && sg.lds_off + pieces * 1024 > p.zero_off) return -1;
+    end = std::max(end, sg.lds_off + pieces * 1024);
+    if (sg.kind == 0) {                               // window row of a staged pixel: the kernel's float form
+      const float inv_row = 1.0f / (float)sg.wrow;
+      for (int pix = 0; pix < sg.npix; ++pix)
+        if ((int)(((float)pix + 0.5f) * inv_row) != pix / sg.wrow) return -1;
+    }
+    const int nk = (sg.kind == 0 ? 9 : 1) * sg.C / 16;
+    const int cpt = sg.C >> 4;
+    for (int t = 0; t < p.tiles_pf; ++t) {
+      const int r0 = t * PX, npx = std::min(PX, hw - r0), y_first = r0 / p.Wo;
+      for (int pp = 0; pp < PX; ++pp) {
+        const int pq = pp < npx ? pp : 0;
+        int pos = pq;
+        if (sg.kind == 0) {
+          const int r = r0 + pq, y = r / p.Wo, x = r - y * p.Wo;
+          pos = (y - y_first) * sg.wrow + x;
+        }
+        for (int kk = 0; kk < nk; ++kk) {
+          const int tap = kk / cpt, c16 = kk - tap * cpt;
+          const int tpos = sg.kind == 0 ? pos + (tap / 3) * sg.wrow + tap % 3 : pos;
+          if (tpos >= sg.npix || (c16 >> 3) >= sg.planes) return -1;
+          const int off = (c16 >> 3) * sg.npix * PP + (c16 & 7) * 32;
+          end = std::max(end, sg.lds_off + tpos * PP + off + 16 + 16);  // ds_read_b128 of lane half lh = 1
+        }
+      }
+    }
+  }
+  return end;
+}
+
 bool conv_burst_plan(const ConvParams& cp, int B, BurstParams* out) {
   using namespace burst;
   BurstParams p{};
@@ -322,6 +371,8 @@ bool conv_burst_plan(const ConvParams& cp, int B, BurstParams* out) {
   off += ZERO_BYTES;
   p.lds = std::max(off, NW * PART);
   if (p.lds > LDS_MAX) return false;
+  p.lds_end = conv_burst_lds_extent(p);
+  if (p.lds_end < 0 || p.lds_end > p.lds) return false;
   p.bias = cp.bias;
   p.act = cp.act;
   p.out = cp.out;
@@ -375,7 +426,7 @@ int launch_conv_burst(const BurstParams* const* ps, int n, int dtype, hipStream_
   int wg = 0, lds = 0, kpw = 0;
   for (int k = 0; k < n; ++k) {
     const BurstParams& p = *ps[k];
-    if (!p.w || !p.out || p.nseg < 1 || p.lds > LDS_MAX || !burst_kpw(p.nk16)) {
+    if (!p.w || !p.out || p.nseg < 1 || p.lds > LDS_MAX || !burst_kpw(p.nk16) || p.lds_end <= 0 || p.lds_end > p.lds) {
       set_error("conv_burst: inconsistent layer");
       return 1;
     }

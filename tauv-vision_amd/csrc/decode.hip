@@ -542,8 +542,8 @@ constexpr int kMaxScanTiles = 4096;                   // tiles per image
 constexpr uint64_t kZeroKey = (0x80000000ull << 32) | 0xFFFFFFFFull;  // largest key of score +0.0
 
 struct ScanWs {
-  uint32_t* img_cnt;  // [B] keys appended so far (zero between calls)
-  uint32_t* ticket;   // [B] tiles finished (zero between calls)
+  uint32_t* img_cnt;  // image b's keys appended so far at [2b] (zero between calls)
+  uint32_t* ticket;   // image b's tiles finished at [2b] (zero between calls)
   uint64_t* keys;     // [B][tiles * kScanElems] the image's appended keys
   int tiles;          // per image
   uint32_t N;         // C * H * W
@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(5,
   // write-through stores (read by whichever workgroup of the image finishes last)
   if (threadIdx.x == 0) {
     const uint32_t kept = kd ? keep_cnt : nk;
-    seg_base = kept ? __hip_atomic_fetch_add((gu32*)(w.img_cnt + b), kept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+    seg_base = kept ? __hip_atomic_fetch_add((gu32*)(w.img_cnt + 2 * b), kept, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                     : 0u;
   }
   __syncthreads();
@@ -1103,16 +1103,16 @@ __global__ __launch_bounds__(kScanThreads) __attribute__((amdgpu_waves_per_eu(5,
   __syncthreads();
   DSTAMP(stamps, 4);
   if (threadIdx.x == 0)
-    last_flag = __hip_atomic_fetch_add((gu32*)(w.ticket + b), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_flag = __hip_atomic_fetch_add((gu32*)(w.ticket + 2 * b), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (last_flag != (uint32_t)(w.tiles - 1)) return;  // workgroup-uniform
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: every key load below is sc1
-  if (threadIdx.x == 0) seg_base = __hip_atomic_load((gu32*)(w.img_cnt + b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) seg_base = __hip_atomic_load((gu32*)(w.img_cnt + 2 * b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const int n = (int)seg_base;
   if (threadIdx.x == 0) {
-    __hip_atomic_store((gu32*)(w.img_cnt + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gu32*)(w.ticket + b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(w.img_cnt + 2 * b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu32*)(w.ticket + 2 * b), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   DSTAMP(stamps, 5);
   fused_select<kScanThreads>(krs, n, b, heat, s0, s1, s2, s3, H, W, K, w.N, ssh, reinterpret_cast<char*>(tile), &ncand,
@@ -1213,8 +1213,15 @@ TileGeom scan_geom(int C, int H, int W, int chan_fast) {
 }
 }  // namespace
 
-// [B] key counts + [B] tickets (zero between calls), then [B][tiles][kScanElems] keys
-size_t decode_head_bytes(int B) { return ((size_t)B * 8 + 255) / 256 * 256; }
+// Head: per image b a key count (word 2b) and a ticket (word 2b + 1) at a FIXED offset for every
+// image a launch can take (B <= 65535), so the counters never move with B or the heatmap geometry
+// and no call's keys land on them: a workspace zero-filled once stays valid for any later call
+// that fits it (each call leaves every counter it used at zero). Then [B][tiles][kScanElems] keys.
+constexpr int kMaxDecodeB = 65535;
+size_t decode_head_bytes(int B) {
+  (void)B;
+  return (size_t)(kMaxDecodeB + 1) * 8;
+}
 size_t decode_workspace_bytes(int B, int C, int H, int W, int K) {
   (void)K;
   const TileGeom g = scan_geom(C, H, W, 1);
@@ -1231,7 +1238,7 @@ int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, i
   if (ws_bytes < decode_workspace_bytes(B, C, H, W, K)) { set_error("decode workspace too small"); return 1; }
   const TileGeom g = scan_geom(C, H, W, st[1] < st[3] ? 1 : 0);
   const int tiles = g.ncg * g.nth * g.ntw;
-  if (tiles > kMaxScanTiles || B > 65535) { set_error("decode: heatmap too large (tiles per image)"); return 1; }
+  if (tiles > kMaxScanTiles || B > kMaxDecodeB) { set_error("decode: heatmap too large (tiles per image)"); return 1; }
   // the tile (+ halo) in fp32, later reused for the tile's compacted keys (at most one per tile
   // element) and the select's lists (top: K rounded up to a power of two; candidates)
   int P = 1;
@@ -1240,8 +1247,8 @@ int launch_decode(const float* heat, const int64_t st[4], int B, int C, int H, i
                                (size_t)g.cg * g.th * g.tw * sizeof(uint64_t),
                                (size_t)(std::max(P, 2) + std::max(K, kRankCap) + 2) * sizeof(uint64_t)});
   ScanWs w;
-  w.img_cnt = (uint32_t*)ws;
-  w.ticket = w.img_cnt + B;
+  w.img_cnt = (uint32_t*)ws;  // image b: img_cnt[2b], ticket[2b] (stride 2: decode_head_bytes)
+  w.ticket = w.img_cnt + 1;
   w.keys = (uint64_t*)((char*)ws + decode_head_bytes(B));
   w.tiles = tiles;
   w.N = (uint32_t)n;

@@ -275,6 +275,56 @@ int diag_conv_burst(const void* const* src, const int* geom, int nseg, int B, in
   return TV_OK;
 }
 
+// conv_burst_plan() for a layer geometry, host only (no device memory, no launch): geom as
+// diag_conv_burst; out[0..3] = representable (1 / 0), the launch's dynamic LDS bytes, the extent of
+// the kernel's LDS accesses (conv_burst_lds_extent: <= the former whenever representable) and the
+// LDS bytes the layer's staging would need (set even when the plan refuses it).
+int diag_burst_plan(const int* geom, int nseg, int B, int Ho, int Wo, int N, int* out) {
+  if (!geom || !out || nseg < 1 || nseg > kBurstMaxSeg || B < 1 || Ho < 1 || Wo < 1 || N < 1) {
+    set_error("diag_burst_plan: bad argument");
+    return TV_EINVAL;
+  }
+  const int BK = 64;
+  static const char dummy[16] = {};
+  ConvParams p{};
+  int kbase = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const int* g = geom + 6 * k;
+    const int H = g[0], W = g[1], C = g[2], ldc = g[3], kk = g[4], st = g[5];
+    if (H < 1 || W < 1 || C < 1 || ldc < C || (kk != 1 && kk != 3) || st < 1) {
+      set_error("diag_burst_plan: bad segment");
+      return TV_EINVAL;
+    }
+    const int ks = (kk * kk * C + BK - 1) / BK;
+    p.seg[k] = ConvSegment{dummy, H, W, C, ldc, kk, kk, st, kk / 2, kk / 2, ks, kbase};
+    kbase += ks;
+  }
+  p.nseg = nseg;
+  p.Ho = Ho;
+  p.Wo = Wo;
+  p.M = B * Ho * Wo;
+  p.N = N;
+  p.Kpad = kbase * BK;
+  p.act = 1;
+  p.out = (void*)dummy;
+  p.out_ldc = (N + 7) / 8 * 8;
+  BurstParams bp{};
+  const bool ok = conv_burst_plan(p, B, &bp);
+  out[0] = ok ? 1 : 0;
+  out[1] = ok ? bp.lds : 0;
+  out[2] = ok ? bp.lds_end : 0;
+  // the staging the layer would need (what the plan compares with the 160 KiB LDS)
+  int need = 0;
+  const int out_rows = std::min(Ho, (64 + Wo - 1) / Wo + 1);
+  for (int k = 0; k < nseg; ++k) {
+    const int* g = geom + 6 * k;
+    const int npix = g[4] == 3 ? (out_rows + 2) * (Wo + 2) : 64;
+    need += ((g[2] + 127) / 128 * npix * 17 + 63) / 64 * 1024;
+  }
+  out[3] = need + 256;
+  return TV_OK;
+}
+
 // One ConvTranspose2d(3, stride 2, padding 1, output_padding 1) + bias + activation through convt3.hip
 // (the engine's kernel for the protonet up-sampling, masknet.py:21,33): src compute dtype NHWC
 // [B, H, W, ldc] (C channels); weight host fp32 [C][N][3][3] (nn.ConvTranspose2d layout); bias host

@@ -7,6 +7,6 @@ from .centernet import (CenterpointDLA34, Centernet, Prediction, get_head_channe
                         preprocess)
 from .dla import DLABackbone  # noqa: F401
 from .decode import (Detection, KeypointDetection, angle_decode, angle_get_bins, decode,  # noqa: F401
-                     decode_keypoints, depth_decode, heatmap_detect, heatmap_nms)
+                     decode_keypoints, decode_records, depth_decode, heatmap_detect, heatmap_nms)
 
 __version__ = "0.1.0"

@@ -80,6 +80,7 @@ EXPORTS = {
     "tv_diag_conv1x1": ([c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp], c_i32),
     "tv_diag_conv_burst": ([c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_i32,
                             c_vp], c_i32),
+    "tv_diag_burst_plan": ([ctypes.POINTER(c_i32), c_i32, c_i32, c_i32, c_i32, c_i32, ctypes.POINTER(c_i32)], c_i32),
     "tv_last_error": ([], ctypes.c_char_p),
     "tv_version": ([], ctypes.c_char_p),
 }

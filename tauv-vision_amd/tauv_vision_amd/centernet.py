@@ -8,6 +8,7 @@ csrc/planner.cpp) and returns the reference's `Prediction`, whose tensors are ch
 slices of one fp32 NHWC head tensor (same shapes and values, different strides).
 """
 import ctypes
+import threading
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -19,6 +20,8 @@ from .config import ObjectConfigSet
 from .dla import DLABackbone, populate
 from .engine import NativeEngine
 from .weights import model_desc, dla34_desc, param_layout
+
+_GRAPH_LOCK = threading.RLock()  # the forward graph cache's launches and captures (all models)
 
 
 @dataclass
@@ -96,12 +99,17 @@ class _NativeModel(nn.Module):
         self.precision = precision
         self._version = [0]
         self._engines = {}
+        # hipGraph replay behind forward()/forward_frames(): a (kind, shape) seen before is replayed
+        # from a captured graph instead of launched op by op (set False for eager launches only)
+        self.graph_replay = True
+        self._graphs = {}
         self.register_load_state_dict_post_hook(lambda module, keys: module.invalidate())
 
     # -- engine cache ---------------------------------------------------------------
     def invalidate(self):
         self._version[0] += 1
         self._engines = {}
+        self._graphs = {}
 
     def _apply(self, fn, *args, **kwargs):
         r = super()._apply(fn, *args, **kwargs)
@@ -135,6 +143,56 @@ class _NativeModel(nn.Module):
             self._engines = {key: eng}
         return eng
 
+    # -- graph cache ------------------------------------------------------------------
+    def _launch(self, eng: NativeEngine, kind: str, x: torch.Tensor) -> torch.Tensor:
+        """One engine forward of `x` (kind "f32": normalised NCHW, "u8": NHWC frames) on the caller's
+        stream, returning a fresh fp32 NHWC head tensor. Per (caller stream, kind, shape): the first
+        call runs eagerly; the second captures the forward once as a hipGraph on a private stream
+        (static input / output buffers, the engine workspace keyed to that stream: an eager warm-up
+        there, then the capture); every later call copies the input in, replays the graph on the
+        caller's stream and returns a copy of the output — so results never alias a later call's,
+        as the reference's fresh tensors. Eager when graph_replay is off, while the caller's stream
+        is capturing, or if the capture failed (graph_failures). Threads (rospy runs one callback
+        thread per camera, centernet_node.py:58-65): launches are enqueued under one lock, so a
+        capture never sees another thread's launches; the GPU work of different streams still
+        overlaps."""
+        fwd = eng.forward_u8 if kind == "u8" else eng.forward
+        if not self.graph_replay or torch.cuda.is_current_stream_capturing():
+            return fwd(x)
+        cur = torch.cuda.current_stream(eng.device)
+        key = (id(eng), eng.generation, cur.cuda_stream, kind, tuple(x.shape))
+        with _GRAPH_LOCK:
+            ent = self._graphs.get(key)
+            if ent is None:  # first sight: eager (the node's warm-up forward, centernet_node.py:50)
+                self._graphs = {k: v for k, v in self._graphs.items() if k[0] == id(eng) and k[1] == eng.generation}
+                self._graphs[key] = {"graph": None, "failed": False}
+                return fwd(x)
+            if ent["failed"]:
+                return fwd(x)
+            if ent["graph"] is None:
+                try:
+                    side = torch.cuda.Stream(eng.device)
+                    inp = torch.empty_like(x, memory_format=torch.contiguous_format)
+                    out = eng.alloc_out(x.shape[0])
+                    side.wait_stream(cur)
+                    with torch.cuda.stream(side):
+                        inp.copy_(x)
+                        fwd(inp, out)  # workspace for (side, B) made outside the capture
+                        graph = torch.cuda.CUDAGraph()
+                        with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
+                            fwd(inp, out)
+                    cur.wait_stream(side)
+                    ent.update(graph=graph, stream=side, inp=inp, out=out)
+                except RuntimeError as e:  # keep the model usable: this (kind, shape) stays eager
+                    import warnings
+                    warnings.warn(f"tauv_vision_amd: hipGraph capture failed ({e}); eager launches for {key[3:]}")
+                    ent["failed"] = True
+                    self.graph_failures = getattr(self, "graph_failures", 0) + 1
+                    return fwd(x)
+            ent["inp"].copy_(x)
+            ent["graph"].replay()
+            return ent["out"].clone()
+
     # -- reference API --------------------------------------------------------------
     def forward(self, img: torch.Tensor) -> Prediction:
         if img.dim() != 4 or img.shape[1] != 3:
@@ -142,7 +200,7 @@ class _NativeModel(nn.Module):
         dev = self._device_for(img)
         img = img.to(dev, torch.float32).contiguous()
         eng = self.engine(dev, img.shape[2], img.shape[3])
-        return prediction_from_nhwc(eng.forward(img), self.object_config)
+        return prediction_from_nhwc(self._launch(eng, "f32", img), self.object_config)
 
     def forward_frames(self, frames: torch.Tensor, size=None) -> Prediction:
         """Raw uint8 RGB camera frames [B, H, W, 3] (or [H, W, 3]) through the node's
@@ -159,8 +217,8 @@ class _NativeModel(nn.Module):
         in_h, in_w = (frames.shape[1], frames.shape[2]) if size is None else (int(size[0]), int(size[1]))
         eng = self.engine(dev, in_h, in_w)
         if (in_h, in_w) == (frames.shape[1], frames.shape[2]):
-            return prediction_from_nhwc(eng.forward_u8(frames), self.object_config)
-        return prediction_from_nhwc(eng.forward(preprocess(frames, in_h, in_w)), self.object_config)
+            return prediction_from_nhwc(self._launch(eng, "u8", frames), self.object_config)
+        return prediction_from_nhwc(self._launch(eng, "f32", preprocess(frames, in_h, in_w)), self.object_config)
 
     def detect(self, frames: torch.Tensor, model_config, n_detections: int = 100, score_threshold: float = 0.3):
         """detect(frames) == decode(forward(preprocess(frames)), ...): camera frames of any size,

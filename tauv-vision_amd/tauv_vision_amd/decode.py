@@ -15,6 +15,7 @@ Differences from the reference:
     while C*H*W < 2^24).
 """
 import ctypes
+import threading
 from dataclasses import dataclass
 from math import atan2, pi
 from typing import List, Optional, Tuple
@@ -140,17 +141,58 @@ class DeviceDecoder:
         return self.records, self.counts
 
 
+_DECODERS = {}  # (device, B, C, H, W, K) -> (DeviceDecoder, pinned host mirror of its packed buffer)
+_DECODERS_LOCK = threading.Lock()
+_DECODERS_MAX = 8
+
+
+def _decoder(dev, B, C, H, W, K):
+    key = (dev.index, B, C, H, W, K)
+    ent = _DECODERS.get(key)
+    if ent is None:
+        if len(_DECODERS) >= _DECODERS_MAX:
+            _DECODERS.pop(next(iter(_DECODERS)))
+        dec = DeviceDecoder(B, C, H, W, K, dev)
+        ent = (dec, torch.empty(dec.packed.numel(), dtype=torch.uint8, pin_memory=True))
+        _DECODERS[key] = ent
+    return ent
+
+
+def _records_many(calls):
+    """Run several device decodes back to back on the current stream, each into a cached decoder
+    (static workspace and records: no allocation or zero fill per call), copy every packed record
+    buffer to pinned host memory and synchronise ONCE. calls: (heat, size, offset, depth, K, mode,
+    ratio, in_h, in_w, thr, aux) tuples; returns [(records [B,K,10], counts [B])] host numpy."""
+    with _DECODERS_LOCK:
+        outs = []
+        for heat, size, offset, depth, K, mode, ratio, in_h, in_w, thr, aux in calls:
+            heat = _gpu(heat, "heatmap")
+            B, C, H, W = heat.shape
+            dec, host = _decoder(heat.device, B, C, H, W, K)
+            dec(heat, size, offset, depth, mode, ratio, in_h, in_w, thr, aux)
+            host.copy_(dec.packed, non_blocking=True)
+            outs.append((host, B, K))
+        torch.cuda.current_stream(heat.device).synchronize()
+        res = []
+        for host, B, K in outs:
+            a = host.numpy()
+            records = a[:B * K * REC * 4].view(np.float32).reshape(B, K, REC).copy()
+            counts = a[B * K * REC * 4:].view(np.int32).copy()
+            res.append((records, counts))
+        return res
+
+
 def _records(heat, size, offset, depth, K, mode, ratio, in_h, in_w, thr, aux=None):
     """Run the device decode; returns host numpy records [B,K,10] and counts [B] (one D2H copy)."""
-    heat = _gpu(heat, "heatmap")
-    B, C, H, W = heat.shape
-    dec = DeviceDecoder(B, C, H, W, K, heat.device)
-    rec, cnt = dec(heat, size, offset, depth, mode, ratio, in_h, in_w, thr, aux)
-    packed = torch.cat((rec.reshape(-1), cnt.view(torch.float32)))
-    host = packed.cpu().numpy()
-    records = host[:B * K * REC].reshape(B, K, REC)
-    counts = host[B * K * REC:].view(np.int32)
-    return records, counts
+    return _records_many([(heat, size, offset, depth, K, mode, ratio, in_h, in_w, thr, aux)])[0]
+
+
+def decode_records(prediction, model_config, n_detections: int, score_threshold: float):
+    """decode() without the per-detection Python objects: host numpy records [B, K, 10] (label,
+    score, y, x, h, w, depth, flat index, -, -; the first counts[b] rows of image b valid) and counts
+    [B] int32 — one device decode, one D2H copy, one host synchronisation."""
+    return _records(prediction.heatmap, prediction.size, prediction.offset, prediction.depth, n_detections, 0,
+                    model_config.downsample_ratio, model_config.in_h, model_config.in_w, score_threshold)
 
 
 def decode(prediction, model_config, n_detections: int, score_threshold: float) -> List[List[Detection]]:
@@ -169,11 +211,13 @@ def decode_keypoints(prediction, model_config, object_config, M_projection, n_de
     """decode.py:51-176: objects (no offset / ratio, depth = 1/sigmoid) and keypoints from
     the GPU; the greedy affinity-angle matching (decode.py:100-135) runs on the host over
     at most K x K_kp records. `keypoint_angle_threshold` is unused, as in the reference."""
-    obj, obj_n = _records(prediction.heatmap, prediction.size, None, prediction.depth, n_detections, 1,
-                          model_config.downsample_ratio, model_config.in_h, model_config.in_w, score_threshold)
-    kp, kp_n = _records(prediction.keypoint_heatmap, prediction.size, None, None, keypoint_n_detections, 1,
-                        model_config.downsample_ratio, model_config.in_h, model_config.in_w,
-                        keypoint_score_threshold, aux=prediction.keypoint_affinity)
+    # both decodes launched back to back, one host synchronisation
+    (obj, obj_n), (kp, kp_n) = _records_many([
+        (prediction.heatmap, prediction.size, None, prediction.depth, n_detections, 1,
+         model_config.downsample_ratio, model_config.in_h, model_config.in_w, score_threshold, None),
+        (prediction.keypoint_heatmap, prediction.size, None, None, keypoint_n_detections, 1,
+         model_config.downsample_ratio, model_config.in_h, model_config.in_w, keypoint_score_threshold,
+         prediction.keypoint_affinity)])
     out = []
     for b in range(obj.shape[0]):
         dets = []

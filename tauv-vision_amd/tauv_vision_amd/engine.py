@@ -45,6 +45,7 @@ class NativeEngine:
                 rc = L.tv_engine_create(ctypes.byref(desc), views, len(host), device_index, ctypes.byref(handle))
             _lib.check(rc, "engine create")
         self._h = handle
+        self.generation = 0  # bumped by trim(): graphs captured before it reference freed workspaces
         del keep, host
 
     def __del__(self):
@@ -75,6 +76,7 @@ class NativeEngine:
     def trim(self):
         """Free every cached (stream, batch) workspace (synchronises the device)."""
         _lib.check(_lib.lib().tv_engine_trim(self._h), "trim")
+        self.generation += 1
 
     def forward(self, img, out=None):
         """img: fp32 NCHW on this device; returns the fp32 NHWC head tensor."""

@@ -297,3 +297,27 @@ def test_decode_graph_replay():
         r2, c2 = ref(heat, size, offset, None, 0, 4, 480, 640, 0.3)
         assert torch.equal(got_c, c2.cpu())
         assert torch.equal(got_r.nan_to_num(-7.0), r2.cpu().nan_to_num(-7.0))
+
+
+def test_decode_workspace_shared_across_batch_sizes_and_geometries():
+    """One zero-filled workspace, sized for the largest call, serves calls at other B and heatmap
+    geometries in any order (the per-image counters sit at fixed offsets, so a smaller-B call's
+    keys never land on a larger-B call's counters): B=8, B=2, another geometry, B=8 again."""
+    from tauv_vision_amd.decode import DeviceDecoder
+    dev = torch.device("cuda")
+    calls = [(8, 4, 120, 160, 100), (2, 4, 120, 160, 100), (3, 2, 200, 96, 300), (8, 4, 120, 160, 100)]
+    decs = [DeviceDecoder(*c, dev) for c in calls]
+    shared = torch.zeros(max(d.ws_bytes for d in decs), dtype=torch.uint8, device=dev)
+    for i, ((B, C, H, W, K), dec) in enumerate(zip(calls, decs)):
+        dec.ws, dec.ws_bytes = shared, shared.numel()
+        g = torch.Generator().manual_seed(900 + i)
+        logits = torch.randn((B, C, H, W), generator=g) * 2.5
+        size = torch.randn((B, H, W, 2), generator=g)
+        offset = torch.rand((B, H, W, 2), generator=g)
+        rec, cnt = dec(logits.cuda(), size.cuda(), offset.cuda(), None, 0, 4, 4 * H, 4 * W, 0.0)
+        rec = rec.cpu().numpy()
+        ref_s, ref_i = _tie_rule_topk(oracle.heatmap_nms(torch.sigmoid(logits), 3).reshape(B, -1).numpy(), K)
+        np.testing.assert_array_equal(rec[..., 7].astype(np.int64), ref_i)
+        np.testing.assert_allclose(rec[..., 1], ref_s, rtol=0, atol=1e-6)
+        assert (cnt.cpu().numpy() == K).all()
+    assert int(shared[:8 * 8].view(torch.int32).abs().sum()) == 0, "counters not left at zero"

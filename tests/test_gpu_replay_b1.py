@@ -1,8 +1,10 @@
 """BASELINE config 2 (the latency path) as bench.py times it: the B=1 step — forward_u8 + device
 decode + async D2H of the records — captured once as a hipGraph and replayed (bench.py
 latency_b1). At B=1 the engine runs its latency-path schedule (engine.cpp make_workspace: ops by
-dependency level, grouped conv_lat / convt_add launches, conv_lat split-K slabs whose tickets a
-memset node zeroes at the start of every replay). Checked here, for the R18 step in fp16 and bf16
+dependency level, grouped conv_lat / convt_add launches, conv_lat split-K slabs whose tickets are
+self-resetting: zeroed once when the workspace is made, and each tile's last-arriving slice zeroes
+its own ticket, so every complete replay leaves them at zero for the next — no memset node, which
+on this ROCm did not re-run correctly on replay). Checked here, for the R18 step in fp16 and bf16
 and the DLA-34 step in fp16:
 
   * three replays, each after the heads, records and counts were clobbered (NaN / -1), reproduce

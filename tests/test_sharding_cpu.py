@@ -47,7 +47,9 @@ def worker(rank, world, port, n, q):
             rec[i] = torch.from_numpy(r)
             cnt[i] = c
         g = RecordGather(per, K, "cpu")
-        all_rec, all_cnt = g(rec, cnt)
+        buf = g(RecordGather.pack(rec, cnt))  # one collective: records + counts in one buffer
+        assert buf.shape == (world, (per * K * REC + per) * 4)
+        all_rec, all_cnt = g.unpack()
         if rank == 0:
             q.put((all_rec[:n].numpy().copy(), all_cnt[:n].numpy().copy()))
     finally:
@@ -128,7 +130,9 @@ def e2e_worker(rank, world, port, q):
             for i, dets in enumerate(oracle.decode(pred, E2E["H"], E2E["W"], E2E["ds"], K, E2E["thr"])):
                 r, c = _pack(dets, K)
                 rec[i], cnt[i] = torch.from_numpy(r), c
-        all_rec, all_cnt = RecordGather(per, K, "cpu")(rec, cnt)
+        g = RecordGather(per, K, "cpu")
+        g(RecordGather.pack(rec, cnt))
+        all_rec, all_cnt = g.unpack()
         if rank == 0:
             q.put((all_rec[:n].numpy().copy(), all_cnt[:n].numpy().copy()))
     finally:

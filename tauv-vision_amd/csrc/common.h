@@ -214,7 +214,10 @@ struct DcnParams {
   int out_ldc, N;
 };
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad);
-int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, hipStream_t s);  // dcn64_mode: 64-channel k-steps when C % 64 == 0
+// dcn64_mode: 0 dcn_gemm; 1 64-channel k-steps when C % 64 == 0 (dcn_gemm64); 2 the same on 64-pixel
+// tiles; 3 the LDS-window kernel (dcn_win) where dcn_win_supported, else as 1
+int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, int cu_count, hipStream_t s);
+bool dcn_win_supported(const DcnParams& p);
 // targets.hip: training targets of the loss (loss.py:31-135)
 int launch_train_heatmap(const uint8_t* valid, const long long* label, const float* center, int B, int n_obj, int L,
                          int in_h, int in_w, int ratio, double sigma, float* out, hipStream_t s);

@@ -33,6 +33,8 @@ constexpr int kOOB = 0x7ff00000;          // buffer offset past any num_records 
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 __device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
+                                    int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
 __device__ __forceinline__ uint4 to_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
 template <typename T>
@@ -493,6 +495,330 @@ __global__ __launch_bounds__(NT, (min_blocks2<BN, PX>())) void dcn_gemm64(const 
     }
 }
 
+// ---- window variant (C == N == 64: DLA-34's 120x160 DeformConvs, node_k of ida_2 / ida_up, two
+// thirds of its DCN time). dcn_gemm64 gathers every corner from L1/L2: 9 taps x 4 corners x 128 B
+// per pixel, ~15 TB/s of useful bytes, the TA/TD rate of 16-byte gathers (MI355X_MICROARCH.md,
+// indexed rows). The corners of a tile's samples lie within a few pixels of the tile (the offsets
+// are a smooth learned field: |offset| <= 1.6 on every DLA-34 layer at the bench weights), so here:
+//  * a persistent 512-thread workgroup per CU walks 16 x 16-pixel tiles; the tile's input window
+//    (rows / columns -1 - MG .. 16 + MG around it, 64 channels, 128-B pixel rows, 16-byte chunks
+//    XOR-swizzled by the window pixel) moves into LDS ONCE per tile by LDS-DMA (out-of-image pixels
+//    read as buffer-OOB zeros), and every corner inside it is read from LDS (ds_read_b128: 4x the
+//    per-CU rate of the L1 gathers); a corner outside the window but inside the image (offsets past
+//    MG) is gathered from global memory in a branch taken only by waves that have one;
+//  * the DeformConv2d weights of all 9 taps (64 x 576, 72 KiB) stay resident in LDS;
+//  * wave w owns tile pixels 32 w .. 32 w + 31 x all 64 output channels: lane (l32, lh) computes its
+//    pixel's sampling state per tap and blends the 16-byte chunk 2 j + lh of each 16-deep sub-step
+//    j straight into the MFMA B operand register (no LDS round trip, no per-k-step barrier);
+//  * one barrier per tile (the window), and the next tile's window DMA is issued as soon as the last
+//    tap's corners are read, under that tap's MFMAs and the epilogue.
+// Same sampling expressions, blend arithmetic, K order and MFMA sequence as dcn_gemm64: the
+// results are bit-identical to it (tests/test_gpu_dcn.py).
+#if defined(TV_DCN_STAMPS)  // stamp build (EXTRA=-DTV_DCN_STAMPS=1, tools/dcn_stamps.py): per-wave cycle buckets
+#define WSTAMP(B)                                                                      \
+  do {                                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    unsigned long long t_;                                                             \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    st_b[B] += t_ - st_last;                                                           \
+    st_last = t_;                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  } while (0)
+#else
+#define WSTAMP(B) \
+  do {            \
+  } while (0)
+#endif
+namespace win {
+constexpr int WNT = 512, TH = 16, TW = 16, MG = 2;
+constexpr int WR = TH + 2 + 2 * MG, WC = TW + 2 + 2 * MG;  // window rows / columns (22 x 22)
+constexpr int WPIX = WR * WC;                               // 484 window pixels
+constexpr int WCHUNKS = WPIX * 8;                           // 16-byte chunks of the window
+constexpr int WPIECES = (WCHUNKS + WNT - 1) / WNT;            // LDS-DMA rounds (8 x 512 chunks)
+constexpr int OFF_W = 0;                                    // weights [9 taps][64 co][128 B]
+constexpr int OFF_X = OFF_W + 9 * 64 * 128;                 // window [WPIECES * 512 chunks][16 B]
+constexpr int OFF_Z = OFF_X + WPIECES * WNT * 16;            // 128 zero bytes: invalid corners
+constexpr int OFF_B = OFF_Z + 128;                          // the 64 biases (fp32)
+constexpr int LDS = OFF_B + 64 * 4;
+static_assert(LDS <= 160 * 1024, "LDS budget");
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+}  // namespace win
+
+template <typename T>
+__global__ __attribute__((amdgpu_flat_work_group_size(win::WNT, win::WNT), amdgpu_waves_per_eu(2, 2))) void dcn_win(
+    const DcnParams p) {
+  using namespace win;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int H = p.H, W = p.W;
+  const int tiles_x = (W + TW - 1) / TW, tiles_f = ((H + TH - 1) / TH) * tiles_x;
+  const int ntot = p.B * tiles_f;
+  // XCD-aware contiguous tile ranges (neighbouring tiles share window rows in the XCD's L2)
+  const int G = gridDim.x, bid = blockIdx.x;
+  int first, stride, end;
+  if ((G & 7) == 0) {
+    first = (int)((long long)ntot * (bid & 7) / 8) + (bid >> 3);
+    end = (int)((long long)ntot * ((bid & 7) + 1) / 8);
+    stride = G >> 3;
+  } else {
+    first = bid;
+    end = ntot;
+    stride = G;
+  }
+  if (first >= end) return;
+
+  i32x4 xr;
+  {
+    const unsigned long long a = (unsigned long long)p.x;
+    xr = i32x4{(int)(unsigned)a, (int)(unsigned)(a >> 32),
+               (int)((unsigned)p.B * H * W * p.ldx * (unsigned)sizeof(T)), 0x00020000};
+  }
+  auto dma = [&](int off, int lds_off) __attribute__((always_inline)) {
+    raw_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(smem + lds_off), 16, off, 0, 0, 0);
+  };
+  // the window of tile t into LDS: chunk g = window pixel g / 8, slot g % 8 holds source chunk
+  // slot ^ swz(pixel) (the reads un-swizzle); chunks past the window land in its slack
+  auto stage = [&](int t) __attribute__((always_inline)) {
+    const int fr = t / tiles_f, r = t - fr * tiles_f, ty = r / tiles_x;
+    const int wy0 = ty * TH - 1 - MG, wx0 = (r - ty * tiles_x) * TW - 1 - MG;
+#pragma unroll
+    for (int q = 0; q < WPIECES; ++q) {
+      const int g = q * WNT + tid;
+      const int wp = g >> 3, c = (g & 7) ^ swz(g >> 3);
+      const int wy = wp / WC, wx = wp - (wp / WC) * WC;
+      const int y = wy0 + wy, x = wx0 + wx;
+      const bool ok = g < WCHUNKS && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      dma(ok ? ((fr * H + y) * W + x) * p.ldx * (int)sizeof(T) + c * 16 : kOOB, OFF_X + (q * WNT + wave * 64) * 16);
+    }
+  };
+
+  // ---- resident: the weights of the 9 taps (row k * 64 + co, chunk c at c ^ swz(row)) and the zeros
+  {
+    const T* w = reinterpret_cast<const T*>(p.w);
+    constexpr int NCH = 9 * 64 * 8 / WNT;
+    uint4 wv[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int g = i * WNT + tid, row = g >> 3, c = g & 7, k = row >> 6, co = row & 63;
+      wv[i] = *reinterpret_cast<const uint4*>(w + (size_t)co * p.Kpad + k * 64 + 8 * c);
+    }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int g = i * WNT + tid, row = g >> 3, c = g & 7;
+      *reinterpret_cast<uint4*>(smem + OFF_W + row * 128 + ((c ^ swz(row)) << 4)) = wv[i];
+    }
+    if (tid < 8) *reinterpret_cast<uint4*>(smem + OFF_Z + tid * 16) = make_uint4(0u, 0u, 0u, 0u);
+    if (tid < 64) reinterpret_cast<float*>(smem + OFF_B)[tid] = p.bias[tid];
+  }
+  // the 27 offset / mask values of this lane's pixel of tile t (32 fp16 = 4 x 16 B: om_ldc >= 32,
+  // 16-byte rows), loaded a tile ahead with the window
+  const int q = 32 * wave + l32;  // this lane's tile pixel
+  i32x4 omr;
+  {
+    const unsigned long long a = (unsigned long long)p.om;
+    omr = i32x4{(int)(unsigned)a, (int)(unsigned)(a >> 32),
+                (int)((unsigned)p.B * H * W * p.om_ldc * (unsigned)sizeof(T)), 0x00020000};
+  }
+  uint4 omv[4];
+  auto load_om = [&](int t) __attribute__((always_inline)) {
+    const int fr = t / tiles_f, r = t - fr * tiles_f, ty = r / tiles_x;
+    const int oy = ty * TH + (q >> 4), ox = (r - ty * tiles_x) * TW + (q & 15);
+    const int off = oy < H && ox < W ? ((fr * H + oy) * W + ox) * p.om_ldc * (int)sizeof(T) : kOOB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) omv[i] = to_u4(raw_buffer_load_v4(omr, off, 16 * i, 0));
+  };
+  auto om_at = [&](int e) __attribute__((always_inline)) -> float {
+    const unsigned d = reinterpret_cast<const unsigned*>(omv)[e >> 1];
+    return (float)__builtin_bit_cast(T, (unsigned short)((e & 1) ? d >> 16 : d & 0xffffu));
+  };
+  stage(first);
+  load_om(first);
+#if defined(TV_DCN_STAMPS)
+  // buckets: 0 tile-top wait, 1 sampling state, 2 corner reads + blend, 3 MFMAs, 4 tap-8 barrier +
+  // next window issue, 5 epilogue, 6 tiles
+  unsigned long long st_b[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_last;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
+
+  for (int t = first; t < end; t += stride) {
+    const int fr = t / tiles_f, r = t - fr * tiles_f, ty = r / tiles_x;
+    const int y0 = ty * TH, x0 = (r - ty * tiles_x) * TW;
+    const int wy0 = y0 - 1 - MG, wx0 = x0 - 1 - MG;
+    const int oy = y0 + (q >> 4), ox = x0 + (q & 15);
+    const bool pval = oy < H && ox < W;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's window pieces and om values landed
+    __syncthreads();                                   // ... and every other thread's window pieces
+    WSTAMP(0);
+#if defined(TV_DCN_STAMPS)
+    st_b[6] += 1;
+#endif
+    float omf[27];
+#pragma unroll
+    for (int e = 0; e < 27; ++e) omf[e] = om_at(e);
+
+    // sampling state of (pixel, tap k), branch-free (dcn_gemm64's expressions and values): corner c
+    // reads LDS at A[c] ^ (chunk << 4) (its window pixel's 128-B row | swizzle << 4, or the zero row
+    // for a corner outside the image) or, outside the window, global memory at go[c]
+    struct St {
+      int A[4], go[4];
+      float wt[4];
+      bool fb;
+    };
+    auto state = [&](int k, St& S) __attribute__((always_inline)) {
+      const float dy = omf[2 * k], dx = omf[2 * k + 1], logit = omf[18 + k];
+      const float mask = 1.0f / (1.0f + expf(-logit));
+      const float py = (float)(oy - 1 + k / 3) + dy;
+      const float px = (float)(ox - 1 + k % 3) + dx;
+      const bool vs = pval && py > -1.f && py < (float)H && px > -1.f && px < (float)W;
+      const float fy = floorf(vs ? py : 0.f), fx = floorf(vs ? px : 0.f);
+      const int yc = (int)fy, xc = (int)fx;
+      const float ly = py - fy, lx = px - fx, hy = 1.f - ly, hx = 1.f - lx;
+      const float w4[4] = {hy * hx, hy * lx, ly * hx, ly * lx};
+      S.fb = false;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int yy = yc + (c >> 1), xx = xc + (c & 1);
+        const bool in = vs && yy >= 0 && yy <= H - 1 && xx >= 0 && xx <= W - 1;
+        const int wy = yy - wy0, wx = xx - wx0;
+        const bool inw = (unsigned)wy < (unsigned)WR && (unsigned)wx < (unsigned)WC;
+        const int wp = wy * WC + wx;
+        S.wt[c] = in ? w4[c] * mask : 0.f;
+        S.A[c] = in && inw ? (OFF_X + wp * 128) | (swz(wp) << 4) : OFF_Z;
+        S.go[c] = in && !inw ? ((fr * H + yy) * W + xx) * p.ldx * (int)sizeof(T) : kOOB;
+        S.fb = S.fb || (in && !inw);
+      }
+    };
+    // the tap's 4 sub-steps x 4 corners: chunk 2 j + lh of each corner (LDS, then the rare global
+    // gathers of corners outside the window: per-lane offsets, no waterfall)
+    auto reads = [&](const St& S, uint4 (&cv)[4][4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          cv[j][c] = *reinterpret_cast<const uint4*>(smem + (S.A[c] ^ ((2 * j + lh) << 4)));
+      if (__builtin_amdgcn_ballot_w64(S.fb) != 0) {  // (wave-uniform)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const uint4 g = to_u4(raw_buffer_load_v4(xr, S.go[c] + (2 * j + lh) * 16, 0, 0));
+            if (S.go[c] != kOOB) cv[j][c] = g;
+          }
+      }
+    };
+    auto blend = [&](const St& S, const uint4 (&cv)[4][4], uint4 (&xf)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        unsigned o[4];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          float a0, a1;
+          if constexpr (std::is_same<T, _Float16>::value) {
+            const unsigned d0 = reinterpret_cast<const unsigned*>(&cv[j][0])[e >> 1];
+            a0 = mix_lo(S.wt[0], d0);
+            a1 = mix_hi(S.wt[0], d0);
+#pragma unroll
+            for (int c = 1; c < 4; ++c) {
+              const unsigned dw = reinterpret_cast<const unsigned*>(&cv[j][c])[e >> 1];
+              a0 = mix_lo_acc(S.wt[c], dw, a0);
+              a1 = mix_hi_acc(S.wt[c], dw, a1);
+            }
+          } else {
+            a0 = 0.f;
+            a1 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              a0 += S.wt[c] * elem<T>(cv[j][c], e);
+              a1 += S.wt[c] * elem<T>(cv[j][c], e + 1);
+            }
+          }
+          o[e >> 1] = pack2<T>(a0, a1);
+        }
+        xf[j] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    };
+
+    f32x16 acc[2] = {f32x16{}, f32x16{}};
+    St S[2];
+    uint4 cv[2][4][4];
+    state(0, S[0]);
+    reads(S[0], cv[0]);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      WSTAMP(1);
+      uint4 xf[4];
+      blend(S[k & 1], cv[k & 1], xf);
+      WSTAMP(2);
+      if (k == 8) {
+        // every wave's corner reads of this tile are done (lgkmcnt): once all waves are here the
+        // window is free, and the next tile's DMA runs under the last MFMAs and the epilogue
+        __syncthreads();
+        if (t + stride < end) {
+          stage(t + stride);
+          load_om(t + stride);
+        }
+        WSTAMP(4);
+      } else {
+        // the next tap's state and corner reads in flight under this tap's MFMAs
+        state(k + 1, S[(k + 1) & 1]);
+        reads(S[(k + 1) & 1], cv[(k + 1) & 1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = k * 64 + 32 * i + l32;
+          const uint4 wf = *reinterpret_cast<const uint4*>(smem + OFF_W + row * 128 + (((2 * j + lh) ^ swz(row)) << 4));
+          Mfma<T>::run(wf, xf[j], acc[i]);
+        }
+      WSTAMP(3);
+    }
+
+    // ---- epilogue (as dcn_gemm64): channel rows (r & 3) + 8 (r >> 2) + 4 lh of block i, pixel l32
+    if (pval) {
+      T* dst = reinterpret_cast<T*>(p.out) + (size_t)((fr * H + oy) * W + ox) * p.out_ldc;
+      const float* lb = reinterpret_cast<const float*>(smem + OFF_B);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int ch = 32 * i + 8 * g + 4 * lh;
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(lb + ch);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float tt = acc[i][4 * g + e] + bb[e];
+            if (p.act == 1) tt = fmaxf(tt, 0.0f);
+            else if (p.act == 2) tt = fmaxf(tt, 0.01f * tt);
+            v[e] = tt;
+          }
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<u32x2*>(dst + ch) = u32x2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+        }
+    }
+    WSTAMP(5);
+  }
+#if defined(TV_DCN_STAMPS)
+  __syncthreads();
+  if (lane == 0) {  // (the stamp build overwrites the output's first bytes)
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(p.out) + ((size_t)bid * 8 + wave) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = st_b[k];
+  }
+#endif
+}
+
+template <typename T>
+static void launch_win(const DcnParams& p, int cu_count, hipStream_t s) {
+  (void)ensure_lds<dcn_win<T>>(win::LDS);
+  const long tiles = (long)p.B * ((p.H + win::TH - 1) / win::TH) * ((p.W + win::TW - 1) / win::TW);
+  int grid = (int)std::min<long>(tiles, cu_count);
+  if (grid >= 8 && tiles > 2L * grid) grid -= grid % 8;
+  hipLaunchKernelGGL((dcn_win<T>), dim3(grid), dim3(win::WNT), win::LDS, s, p);
+}
+
 template <typename T, int BN, int PX>
 static void launch64(const DcnParams& p, hipStream_t s) {
   constexpr int lds = lds_bytes2<BN, PX>();
@@ -510,7 +836,13 @@ bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, 
   return C % dcn::KS == 0 && N % 64 == 0 && ldx % 8 == 0 && om_ldc >= 27 && out_ldc % 4 == 0;
 }
 
-int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, hipStream_t s) {
+bool dcn_win_supported(const DcnParams& p) {
+  return p.C == 64 && p.N == 64 && p.ldx % 8 == 0 && p.out_ldc % 4 == 0 && p.Kpad >= 9 * 64 &&
+         p.om_ldc >= 32 && p.om_ldc % 8 == 0 &&
+         (long)p.B * p.H * p.W * p.ldx * 2 < dcn::kOOB;
+}
+
+int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, int cu_count, hipStream_t s) {
   if (!dcn_gemm_supported((long)p.B * p.H * p.W, p.C, p.N, p.ldx, p.om_ldc, p.out_ldc, p.Kpad) || p.Kpad < 9 * p.C) {
     set_error("dcn_gemm: channels must be multiples of 32 (input) / 64 (output), tensors below 2 GB");
     return 1;
@@ -523,7 +855,10 @@ int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, hipStream_t s
     set_error("dcn_gemm: fp16/bf16 only");
     return 1;
   }
-  if (p.C % 64 == 0 && dcn64_mode) {  // full-line gathers (every DLA-34 DeformConv); mode 2: 64-pixel tiles
+  if (dcn64_mode >= 3 && dcn_win_supported(p)) {  // LDS window (C == N == 64; mode 4: diagnostics only)
+    if (dtype == F16) dcn::launch_win<_Float16>(p, cu_count, s);
+    else dcn::launch_win<__bf16>(p, cu_count, s);
+  } else if (p.C % 64 == 0 && dcn64_mode) {  // full-line gathers (every DLA-34 DeformConv); mode 2: 64-pixel tiles
     // 64-pixel tiles (measured: 4 resident workgroups per CU hide the corner gathers better than
     // 2 of 128 pixels; the 64-channel layers 5561 -> 5775 frames/s at B=64); 128-channel outputs
     // too when 128-pixel tiles would leave few workgroups per CU (B=1: 1.65 -> 1.52 ms; B=64 neutral)

@@ -50,7 +50,7 @@ namespace tv {
 int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int om_ldc, const float* weight,
                   const float* bias, int N, int act, int dtype, int variant, void* out, hipStream_t s) {
   if (!x || !om || !weight || !bias || !out || B < 1 || H < 1 || W < 1 || C < 1 || N < 1 || om_ldc < 27 ||
-      variant < 0 || variant > 3 || dtype < F32 || dtype > BF16 || act < 0 || act > 2) {
+      variant < 0 || variant > 4 || dtype < F32 || dtype > BF16 || act < 0 || act > 2) {
     set_error("diag_dcn_conv: bad argument");
     return TV_EINVAL;
   }
@@ -76,7 +76,7 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
   TV_HIP(hipMalloc(&db.p, hb.size() * 4));
   TV_HIP(hipMemcpy(db.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
   int rc = 0;
-  if (variant < 3) {
+  if (variant < 3 || variant == 4) {
     DcnParams q{};
     q.x = x;
     q.B = B;
@@ -97,7 +97,14 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
       set_error("diag_dcn_conv: dcn_gemm64 needs C % 64 == 0");
       return TV_EINVAL;
     }
-    rc = launch_dcn_gemm(q, dtype, variant, s);
+    if (variant == 4 && !dcn_win_supported(q)) {
+      set_error("diag_dcn_conv: dcn_win needs C == N == 64");
+      return TV_EINVAL;
+    }
+    int dev = 0, cus = 0;
+    TV_HIP(hipGetDevice(&dev));
+    TV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    rc = launch_dcn_gemm(q, dtype, variant == 4 ? 3 : variant, cus, s);
   } else {
     const size_t cols_bytes = (size_t)B * H * W * K * esz;
     TV_HIP(hipMalloc(&dcols.p, cols_bytes));

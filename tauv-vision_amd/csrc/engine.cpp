@@ -1230,7 +1230,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
                     : launch_prep_nchw((const float*)input, ws->B, desc.in_h, desc.in_w, dst, plan.in_cpad, dtype, s);
   }
   if (ws->dcn_skip[i]) return TV_OK;  // sampled inside the next op's fused DCNv2 kernel
-  if (ws->dcn[i].x) return launch_dcn_gemm(ws->dcn[i], dtype, dcn64_mode, s);
+  if (ws->dcn[i].x) return launch_dcn_gemm(ws->dcn[i], dtype, dcn64_mode, cu_count, s);
   if (op.kind == OP_MAXPOOL || op.kind == OP_DCN || op.kind == OP_DWCONVT_ADD) {
     const TensorSpec& src = plan.tensors[op.src];
     const TensorSpec& dst = plan.tensors[op.out];
@@ -1466,7 +1466,9 @@ const char* Engine::op_kernel(int B, size_t i) {
       else if (ws->dcn[i].x) {
         const DcnParams& d = ws->dcn[i];
         const bool wide = d.N % 128 == 0;
-        if (dcn64_mode && d.C % 64 == 0) {  // dcn_gemm64<T, BN, PX>: the pixel tile as launch_dcn_gemm picks it
+        if (dcn64_mode >= 3 && dcn_win_supported(d)) {
+          name = std::string("tv::dcn::dcn_win<") + t + ">";
+        } else if (dcn64_mode && d.C % 64 == 0) {  // dcn_gemm64<T, BN, PX>: the pixel tile as launch_dcn_gemm picks it
           const long tiles128 = ((long)d.B * d.H * d.W + 127) / 128 * (d.N / 128);
           const int px = !wide || dcn64_mode == 2 || tiles128 < 1024 ? 64 : 128;
           name = std::string("tv::dcn::dcn_gemm64<") + t + (wide ? ", 128, " : ", 64, ") + std::to_string(px) + ">";

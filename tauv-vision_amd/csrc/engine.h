@@ -96,7 +96,9 @@ struct Engine {
   int stem_mode = 1;           // fused staging + stem kernel for fp16/bf16 (env TV_STEM=0 off)
   int lat_mode = 1;            // conv_lat.hip for layers whose chosen kernel fills < lat_units work units
                                // (env TV_LAT=0 off)
-  int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (env TV_DCN64=0 off)
+  int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (knob TV_DCN64:
+                               // 0 dcn_gemm, 2 dcn_gemm64 on 64-pixel tiles, 3 the LDS-window dcn_win for C == N == 64:
+                               // bit-equal, measured 194 vs 187 us per 120x160 layer, so not the default)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
   int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1; 2 = N <= 128 only)
   int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)

@@ -10,7 +10,10 @@ identities need no torchvision:
 Inputs and weights are rounded to the compute dtype first, so in the identities the only
 difference left is fp32 accumulation order and the output rounding. Variants: 0 dcn_gemm,
 1 dcn_gemm64, 2 dcn_gemm64 with 64-pixel tiles (same blend arithmetic and K order: bit-equal),
-3 the unfused path (sampling into a column tensor + the implicit-GEMM conv kernel; fp32's path).
+3 the unfused path (sampling into a column tensor + the implicit-GEMM conv kernel; fp32's path),
+4 dcn_win (C == N == 64: the tile's input window staged in LDS, corners outside it gathered from
+global memory; same arithmetic and K order as dcn_gemm64: bit-equal to it — the bilinear case's
+offsets of sigma 2.5 exercise the out-of-window path).
 """
 import ctypes
 
@@ -31,10 +34,11 @@ ULP = {"fp32": 2e-6, "fp16": 1.0e-3, "bf16": 8.0e-3}
 TOL = {"fp32": 2e-5, "fp16": 4e-3, "bf16": 3e-2}
 
 
-def variants(precision, C):
+def variants(precision, C, N=None):
     if precision == "fp32":
         return [3]
-    return [0, 1, 2, 3] if C % 64 == 0 else [0, 3]
+    v = [0, 1, 2, 3] if C % 64 == 0 else [0, 3]
+    return v + [4] if C == 64 and N == 64 else v
 
 
 def dcn_gpu(x, om, w, b, act, precision, variant):
@@ -90,12 +94,12 @@ def test_dcn_zero_offsets_unit_mask_is_conv(precision, shape):
     zero = torch.zeros(B, 9, H, W)
     om = rnd(om_of(zero, zero, torch.full((B, 9, H, W), 30.0)), precision)  # sigmoid(30) == 1.0f
     ref = F.conv2d(x.double(), w.double(), b.double(), padding=1).float()
-    outs = {v: dcn_gpu(x, om, w, b, 0, precision, v) for v in variants(precision, C)}
+    outs = {v: dcn_gpu(x, om, w, b, 0, precision, v) for v in variants(precision, C, N)}
     for v, o in outs.items():
         assert_close(o, ref, ULP[precision], f"variant {v}")
-    fused = [o for v, o in outs.items() if v in (0, 1, 2)]
+    fused = [o for v, o in outs.items() if v in (0, 1, 2, 4)]
     for o in fused[1:]:
-        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 tilings must be bit-identical"
+        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 / dcn_win tilings must be bit-identical"
 
 
 def shifted_conv(x, w, b, dy, dx):
@@ -123,7 +127,7 @@ def test_dcn_integer_offsets_is_shifted_conv(precision, shape):
                torch.full((B, 9, H, W), 30.0))
     om = rnd(om, precision)
     ref = shifted_conv(x, w, b, dy, dx)
-    for v in variants(precision, C):
+    for v in variants(precision, C, N):
         assert_close(dcn_gpu(x, om, w, b, 0, precision, v), ref, ULP[precision], f"variant {v}")
 
 
@@ -135,7 +139,7 @@ def test_dcn_offsets_outside_image_give_bias(precision):
     for sgn in (1.0, -1.0):
         om = rnd(om_of(sgn * far, far, torch.randn(B, 9, H, W, generator=g)), precision)
         want = rnd(b.view(1, N, 1, 1).expand(B, N, H, W), precision)
-        for v in variants(precision, C):
+        for v in variants(precision, C, N):
             got = dcn_gpu(x, om, w, b, 0, precision, v)
             assert torch.equal(got, want), f"variant {v}: samples outside the image must be 0"
         relu = dcn_gpu(x, om, w, b, 1, precision, variants(precision, C)[0])
@@ -153,9 +157,27 @@ def test_dcn_bilinear_vs_oracle_restatement(precision, shape):
                    torch.randn(B, 9, H, W, generator=g) * 2.0), precision)
     off, logit = om[:, :18], om[:, 18:]
     ref = deform_conv2d(x.double(), off.double(), torch.sigmoid(logit.double()), w.double(), b.double()).float()
-    outs = {v: dcn_gpu(x, om, w, b, 1, precision, v) for v in variants(precision, C)}
+    outs = {v: dcn_gpu(x, om, w, b, 1, precision, v) for v in variants(precision, C, N)}
     for v, o in outs.items():
         assert_close(o, ref.clamp_min(0.0), TOL[precision], f"variant {v}")
-    fused = [o for v, o in outs.items() if v in (0, 1, 2)]
+    fused = [o for v, o in outs.items() if v in (0, 1, 2, 4)]
     for o in fused[1:]:
-        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 tilings must be bit-identical"
+        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 / dcn_win tilings must be bit-identical"
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("sigma", [0.7, 4.0])
+def test_dcn_window_kernel_multi_tile_bit_equal(precision, sigma):
+    """dcn_win over several 16 x 16 tiles per frame (partial tiles at the right and bottom edges, the
+    persistent tile loop, the next tile's window staged under the last tap) with offsets mostly inside
+    the window (sigma 0.7) or mostly past it (sigma 4): bit-equal to dcn_gemm64, close to the
+    restated torchvision algorithm."""
+    B, C, H, W, N = 3, 64, 37, 45, 64
+    x, w, b, g = inputs(B, C, H, W, N, precision, 21)
+    om = rnd(om_of(torch.randn(B, 9, H, W, generator=g) * sigma, torch.randn(B, 9, H, W, generator=g) * sigma,
+                   torch.randn(B, 9, H, W, generator=g) * 2.0), precision)
+    got = dcn_gpu(x, om, w, b, 1, precision, 4)
+    assert torch.equal(got, dcn_gpu(x, om, w, b, 1, precision, 1)), "dcn_win must equal dcn_gemm64 bit for bit"
+    off, logit = om[:, :18], om[:, 18:]
+    ref = deform_conv2d(x.double(), off.double(), torch.sigmoid(logit.double()), w.double(), b.double()).float()
+    assert_close(got, ref.clamp_min(0.0), TOL[precision], "dcn_win")

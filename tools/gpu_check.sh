@@ -19,7 +19,7 @@ step tests 900 python -u -m pytest --maxfail=${MAXFAIL:-1} -v --timeout 120 --ti
 grep -E "passed|failed|FAILED|Error" $O/tests.log | tail -6
 BENCH_PROFILE_OUT=$O/ops_r18.json step bench_r18 500 python bench.py ${BENCH_ARGS:-}
 tail -1 $O/bench_r18.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('r18', d['value'], d['ms_per_step'], d.get('launch'), 'eager', d.get('eager_value'), 'frac', d['roofline']['frac'], d['roofline'].get('frac_best'), 'e2e', d['e2e_frac_of_peak'], 'api', d.get('api'), 'node', d.get('node_b1'), 'b1', {k: v['ms_per_frame'] for k, v in (d.get('latency_b1') or {}).items()})"
-for m in dla34 yolact; do
+for m in ${MODELS-dla34 yolact}; do
   BENCH_PROFILE_OUT=$O/ops_$m.json step bench_$m 300 python bench.py --model $m --no-cpu-baseline --no-extras --no-b1
   tail -1 $O/bench_$m.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$m', d['value'], d['ms_per_step'], d.get('launch'), 'eager', d.get('eager_value'), 'frac', d['roofline']['frac'], d.get('mask_roofline', {}).get('achieved'))"
 done

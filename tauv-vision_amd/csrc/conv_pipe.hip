@@ -32,6 +32,10 @@ constexpr int G = GA + GB;                   // LDS-DMA instructions per wave pe
 
 typedef __attribute__((address_space(3))) char lds_char;
 typedef const __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(1))) unsigned gu32;  // global (never flat) agent-scope ticket words
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 
 __device__ __forceinline__ void dma16(const void* src, lds_char* dst_wave_base) {
   __builtin_amdgcn_global_load_lds((gvoid*)src, (__attribute__((address_space(3))) void*)dst_wave_base, 16, 0, 0);
@@ -63,10 +67,16 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): LDS-DMA base in M0
 
-  const int nb = p.mtiles * p.ntiles;
+  // split-K (MODE 0, ksplit > 1): ksplit workgroups per tile, adjacent in the XCD-contiguous order
+  // so a tile's slices tend to share an L2; slice s walks k-steps [ks0, ks1)
+  const int ksplit = MODE == 0 && p.ksplit > 1 ? p.ksplit : 1;
+  const int nb = p.mtiles * p.ntiles * ksplit;
   const int bid = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7;
-  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int lin_s = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int lin = lin_s / ksplit;
+  const int slice = lin_s - lin * ksplit;
+  const int ks0 = (int)((long)p.nks * slice / ksplit);
   const int ntile = lin % p.ntiles;
   const int mtile = lin / p.ntiles;
   const int m0 = mtile * BM;
@@ -96,11 +106,11 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     const int c = (lane & 7) ^ ((row >> 1) & 7);
     wsrc[i] = reinterpret_cast<const T*>(p.weight) + (size_t)(n0 + row) * p.Kpad + c * VEC;
   }
-  const int total_ks = p.nks;
+  const int total_ks = (int)((long)p.nks * (slice + 1) / ksplit) - ks0;
   const void* const zero = p.zero;  // hoisted: the DMA intrinsic is treated as a memory clobber
   // constant address space: the per-k-step descriptor read is a scalar load, not a
   // (vmcnt-counted) vector load that would drain the DMA pipeline
-  const __attribute__((address_space(4))) KStep* kdesc = (const __attribute__((address_space(4))) KStep*)p.ks;
+  const __attribute__((address_space(4))) KStep* kdesc = (const __attribute__((address_space(4))) KStep*)p.ks + ks0;
 
   // Per-segment lane state for uniform-tap k-steps: the lane's base pointer (pixel
   // (b, oy*stride - pad_h, ox*stride - pad_w), its chunk) and a bit mask of the taps that land
@@ -113,6 +123,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   uint32_t woff[GB];
 #pragma unroll
   for (int i = 0; i < GB; ++i) woff[i] = (uint32_t)(wsrc[i] - wbase);
+  wbase += (size_t)ks0 * BK;  // this slice's first k-step
 
   // wave-uniform descriptor: 80 bytes by scalar loads (constant address space), fetched one
   // k-step before its DMA is issued (the prologue's three at once): a cold descriptor is an L2 /
@@ -249,10 +260,12 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     if (ks + 1 < total_ks) step(ks + 1, fb, fa);
   }
 
-  // ---- epilogue: bias + activation into an fp32 staging tile, then 16-byte stores
+  // ---- epilogue: bias + activation into an fp32 staging tile, then 16-byte stores (split-K: the
+  // raw partial tile; bias and activation after the slices are summed)
   __syncthreads();
   float* stg = reinterpret_cast<float*>(smem);
   constexpr int SR = EROW / 4;
+  const bool split = ksplit > 1;
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
 #pragma unroll
@@ -267,7 +280,12 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float x = acc[a][b][4 * g + e] + bias4[e];
+          float x = acc[a][b][4 * g + e];
+          if (split) {
+            v[e] = x;
+            continue;
+          }
+          x += bias4[e];
           if (p.act == 1) x = fmaxf(x, 0.0f);
           else if (p.act == 2) x = x >= 0.0f ? x : 0.01f * x;
           v[e] = x;
@@ -285,6 +303,74 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   const int cc = tid % CPR;
   const int r0 = tid / CPR;
   const int n = n0 + cc * OVEC;
+  if (MODE == 0 && split) {
+    // Split-K hand-off (the conv_lat.hip scheme): the partial tile goes to slab[tile][slice] with
+    // write-through sc1 stores, each wave drains them, the workgroup barrier orders that before one
+    // relaxed agent-scope ticket; the workgroup drawing ksplit - 1 sums the slices in slice order
+    // (its own from LDS, the others by L1-bypassing sc1 loads: bit-identical whichever arrives
+    // last), applies bias + activation, stores, and resets the ticket.
+    constexpr int TILE_F = BM * BN;
+    constexpr int SC1 = 16;
+    i32x4 rs;
+    {
+      const unsigned long long a = (unsigned long long)(p.slab + (size_t)lin * ksplit * TILE_F);
+      rs.x = (int)(unsigned)a;
+      rs.y = (int)(unsigned)(a >> 32);
+      rs.z = ksplit * TILE_F * 4;
+      rs.w = 0x00020000;
+    }
+    constexpr int FCPR = BN / 4, FRSTEP = NT / FCPR, FNP = BM / FRSTEP;
+    const int fcc = tid % FCPR, fr0 = tid / FCPR;
+#pragma unroll
+    for (int k = 0; k < FNP; ++k) {
+      const int row = fr0 + k * FRSTEP;
+      if (m0 + row >= p.M) break;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(stg + row * SR + fcc * 4);
+      raw_buffer_store_v4(__builtin_bit_cast(u32x4, v), rs, ((slice * BM + row) * BN + fcc * 4) * 4, 0, SC1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* last_flag = reinterpret_cast<unsigned*>(smem + LDS - 16);
+    if (tid == 0) *last_flag = __hip_atomic_fetch_add((gu32*)(p.cnt + lin), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*last_flag != (unsigned)(ksplit - 1)) return;  // workgroup-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: every slab load below is sc1
+    const int nf = n0 + fcc * 4;
+    const uint4 braw = gload16(p.bias + nf);
+    const float bias4[4] = {__uint_as_float(braw.x), __uint_as_float(braw.y), __uint_as_float(braw.z),
+                            __uint_as_float(braw.w)};
+    f32x4 sum[FNP];
+    for (int q = 0; q < ksplit; ++q) {
+#pragma unroll
+      for (int k = 0; k < FNP; ++k) {
+        const int row = fr0 + k * FRSTEP;
+        const bool live = m0 + row < p.M;
+        f32x4 a;
+        if (q == slice) a = *reinterpret_cast<const f32x4*>(stg + row * SR + fcc * 4);
+        else
+          a = __builtin_bit_cast(
+              f32x4, raw_buffer_load_v4(rs, live ? ((q * BM + row) * BN + fcc * 4) * 4 : (int)0x80000000u, 0, SC1));
+        sum[k] = q == 0 ? a : sum[k] + a;
+      }
+    }
+    // back through the staging tile so the stores keep the OutT chunking of the plain path
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < FNP; ++k) {
+      const int row = fr0 + k * FRSTEP;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = sum[k][e] + bias4[e];
+        if (p.act == 1) x = fmaxf(x, 0.0f);
+        else if (p.act == 2) x = x >= 0.0f ? x : 0.01f * x;
+        v[e] = x;
+      }
+      *reinterpret_cast<f32x4*>(stg + row * SR + fcc * 4) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store((gu32*)(p.cnt + lin), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (MODE == 0) {
     if (n < p.N) {
 #pragma unroll 4
@@ -343,7 +429,9 @@ template <typename T, typename OutT, int MODE>
 static int launch_pipe_t(const ConvParams& p, const ConvParams* dp, void* out, hipStream_t s) {
   auto k = conv_pipe<T, OutT, MODE>;
   if (int r = ensure_lds<conv_pipe<T, OutT, MODE>>(LDS)) return r;
-  hipLaunchKernelGGL(k, dim3(p.mtiles * p.ntiles), dim3(NT), LDS, s, dp, out);
+  const int ksplit = MODE == 0 && p.ksplit > 1 ? p.ksplit : 1;
+  if (ksplit > 1 && (!p.slab || !p.cnt || ksplit > p.nks)) return 1;  // TV_EINVAL
+  hipLaunchKernelGGL(k, dim3(p.mtiles * p.ntiles * ksplit), dim3(NT), LDS, s, dp, out);
   TV_HIP(hipGetLastError());
   return 0;
 }

@@ -318,6 +318,8 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
     else if (k == "TV_LAT_SPLIT_MIN") lat_split_min_nks = std::max(0, v);
+    else if (k == "TV_PIPE_SPLIT") pipe_split_mode = std::max(0, std::min(2, v));
+    else if (k == "TV_PIPE_SPLIT_MAX") pipe_split_max = std::max(1, std::min(64, v));
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
     else if (k == "TV_CT3") ct3_mode = v ? 1 : 0;
     else if (k == "TV_BURST") burst_mode = std::max(0, std::min(2, v));
@@ -439,6 +441,8 @@ Engine::~Engine() {
     if (kv.second->dparams) (void)hipFree(kv.second->dparams);
     if (kv.second->dks) (void)hipFree(kv.second->dks);
     if (kv.second->slab) (void)hipFree(kv.second->slab);
+    if (kv.second->pslab) (void)hipFree(kv.second->pslab);
+    if (kv.second->pcnt) (void)hipFree(kv.second->pcnt);
     if (kv.second->cnt) (void)hipFree(kv.second->cnt);
     delete kv.second;
   }
@@ -1123,6 +1127,36 @@ int Engine::make_workspace(int B, Workspace* ws) {
       TV_HIP(hipDeviceSynchronize());
     }
   }
+  // conv_pipe split-K (MODE 0) for layers whose 256 x 128 tiles fill a fraction of the CUs: the fp32
+  // path's deep levels at small batches (R18 at B=1: 15x20 / 512-channel 3x3, 2 x 4 tiles of 144
+  // k-steps on 8 of 256 CUs). ksplit workgroups per tile, each slice >= 4 k-steps (the ring depth
+  // plus one), tiles x slices within one round of CUs; partial tiles meet in pslab, tickets in pcnt
+  // (knob TV_PIPE_SPLIT: 0 off, 1 fp32 only, 2 every dtype; TV_PIPE_SPLIT_MAX slices per tile)
+  {
+    size_t slab_floats = 0, tickets = 0;
+    for (size_t i = 0; i < nops; ++i) {
+      ConvParams& p = ws->params[i];
+      const OpSpec& op = plan.ops[i];
+      if (!ws->use_pipe[i] || op.kind == OP_CONVT_ADD || op.up_s) continue;
+      if (!(pipe_split_mode == 2 || (pipe_split_mode == 1 && dtype == F32))) continue;
+      const int tiles = p.mtiles * p.ntiles;
+      int ks = std::min({pipe_split_max, cu_count / std::max(1, tiles), p.nks / 4});
+      p.ksplit = ks > 1 ? ks : 0;
+      if (!p.ksplit) continue;
+      slab_floats = std::max(slab_floats, (size_t)tiles * ks * kPipeTileM * 128);
+      tickets = std::max(tickets, (size_t)tiles);
+    }
+    if (tickets) {
+      TV_HIP(hipMalloc((void**)&ws->pslab, slab_floats * sizeof(float)));
+      TV_HIP(hipMalloc((void**)&ws->pcnt, tickets * sizeof(unsigned)));
+      TV_HIP(hipMemset(ws->pcnt, 0, tickets * sizeof(unsigned)));
+      for (size_t i = 0; i < nops; ++i)
+        if (ws->use_pipe[i] && ws->params[i].ksplit) {
+          ws->params[i].slab = ws->pslab;
+          ws->params[i].cnt = ws->pcnt;
+        }
+    }
+  }
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
@@ -1149,6 +1183,8 @@ int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
     if (ws->dparams) (void)hipFree(ws->dparams);
     if (ws->dks) (void)hipFree(ws->dks);
     if (ws->slab) (void)hipFree(ws->slab);
+    if (ws->pslab) (void)hipFree(ws->pslab);
+    if (ws->pcnt) (void)hipFree(ws->pcnt);
     if (ws->cnt) (void)hipFree(ws->cnt);
     delete ws;
     return rc;
@@ -1167,6 +1203,8 @@ int Engine::trim() {
     if (kv.second->dparams) (void)hipFree(kv.second->dparams);
     if (kv.second->dks) (void)hipFree(kv.second->dks);
     if (kv.second->slab) (void)hipFree(kv.second->slab);
+    if (kv.second->pslab) (void)hipFree(kv.second->pslab);
+    if (kv.second->pcnt) (void)hipFree(kv.second->pcnt);
     if (kv.second->cnt) (void)hipFree(kv.second->cnt);
     delete kv.second;
   }
@@ -1492,7 +1530,10 @@ const char* Engine::op_kernel(int B, size_t i) {
         name = std::string("tv::c1x1::conv1x1_stream<") + t + (op.N > 64 ? ", 4>" : ", 2>");
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ", " + std::to_string(ws->c3_nw[i]) + ">";
-      else if (ws->use_pipe[i]) name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
+      else if (ws->use_pipe[i]) {
+        name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
+        if (ws->params[i].ksplit > 1) name += " split-K " + std::to_string(ws->params[i].ksplit);
+      }
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";
     }
     return name.c_str();

@@ -60,6 +60,8 @@ struct Workspace {
   KStep* dks = nullptr;             // k-step descriptors of all pipelined ops
   float* slab = nullptr;            // conv_lat split-K partial tiles (one region per slot of a grouped launch)
   unsigned* cnt = nullptr;          // conv_lat split-K tickets, one per tile and slot, zeroed per forward
+  float* pslab = nullptr;           // conv_pipe split-K partial tiles (one layer at a time)
+  unsigned* pcnt = nullptr;         // conv_pipe split-K tickets, one per tile (reset by the last slice)
   std::vector<int> level;           // per op: dependency level (the arena's time; plan order when not grouping)
   std::vector<int> order;           // the ops in execution order: by level, then plan order
   std::vector<std::vector<int>> groups;  // the schedule: conv_lat layers of one level in one launch, others alone
@@ -107,6 +109,8 @@ struct Engine {
   int burst_mode = 1;          // conv_burst.hip for the small conv_lat layers it represents (knob TV_BURST=0 off,
                                // 2 = every layer it represents: diagnostics / tests)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)
+  int pipe_split_mode = 1;     // conv_pipe split-K on under-filled layers: 0 off, 1 fp32 only, 2 every dtype (TV_PIPE_SPLIT)
+  int pipe_split_max = 16;     // ... at most this many slices per tile (knob TV_PIPE_SPLIT_MAX)
   int lat_split_min_nks = 32;  // ... for layers of at least this many k-steps (knob TV_LAT_SPLIT_MIN)
   int stamp_op = -1;           // diagnostics: op whose conv3x3 launch gets a stamp buffer (knob TV_C3_STAMPS=op:ptr)
   unsigned long long* stamp_buf = nullptr;

@@ -1,4 +1,4 @@
-// Split-K implicit GEMM for the small pyramid levels (gfx950, fp16 / bf16).
+// Split-K implicit GEMM for the small pyramid levels (gfx950, fp16 / bf16 / fp32).
 //
 // The deep DLA levels (dla.py:79-135 Trees at 30x40 .. 4x5 for a 640x480 frame, their Roots,
 // the IDAUp projections at those levels; centerpoint_dla.py's 256/512-channel levels 4-5) hold a
@@ -355,7 +355,12 @@ __device__ __forceinline__ void conv_lat_tile(const ConvParams* __restrict__ pp,
       if (p.act == 1) v[e] = fmaxf(v[e], 0.0f);
       else if (p.act == 2) v[e] = v[e] >= 0.0f ? v[e] : 0.01f * v[e];
     }
-    store_chunk<T>(out + (size_t)m * p.out_ldc + p.out_coff + n, v);
+    if constexpr (sizeof(T) == 4) {  // fp32: 8 channels are two 16-byte chunks
+      store_chunk<T>(out + (size_t)m * p.out_ldc + p.out_coff + n, v);
+      store_chunk<T>(out + (size_t)m * p.out_ldc + p.out_coff + n + 4, v + 4);
+    } else {
+      store_chunk<T>(out + (size_t)m * p.out_ldc + p.out_coff + n, v);
+    }
   }
 }
 
@@ -415,7 +420,7 @@ int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStr
   }
   if (dtype == F16) return lat::launch_t<_Float16>(p, dp, s);
   if (dtype == BF16) return lat::launch_t<__bf16>(p, dp, s);
-  set_error("conv_lat: fp16/bf16 only");
+  return lat::launch_t<float>(p, dp, s);
   return 1;
 }
 
@@ -439,8 +444,7 @@ int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* 
   }
   if (dtype == F16) return lat::launch_group_t<_Float16>(g, s);
   if (dtype == BF16) return lat::launch_group_t<__bf16>(g, s);
-  set_error("conv_lat: fp16/bf16 only");
-  return 1;
+  return lat::launch_group_t<float>(g, s);
 }
 
 }  // namespace tv

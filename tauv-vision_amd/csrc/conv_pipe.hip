@@ -339,19 +339,22 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     const uint4 braw = gload16(p.bias + nf);
     const float bias4[4] = {__uint_as_float(braw.x), __uint_as_float(braw.y), __uint_as_float(braw.z),
                             __uint_as_float(braw.w)};
-    f32x4 sum[FNP];
-    for (int q = 0; q < ksplit; ++q) {
+    // every slice from the slab, this one included (its own sc1 stores have landed): no per-element
+    // register-or-load select, which would make hipcc branch and wait per load; rows past M read
+    // slab bytes that are never stored
+    int roff[FNP];
 #pragma unroll
-      for (int k = 0; k < FNP; ++k) {
-        const int row = fr0 + k * FRSTEP;
-        const bool live = m0 + row < p.M;
-        f32x4 a;
-        if (q == slice) a = *reinterpret_cast<const f32x4*>(stg + row * SR + fcc * 4);
-        else
-          a = __builtin_bit_cast(
-              f32x4, raw_buffer_load_v4(rs, live ? ((q * BM + row) * BN + fcc * 4) * 4 : (int)0x80000000u, 0, SC1));
-        sum[k] = q == 0 ? a : sum[k] + a;
-      }
+    for (int k = 0; k < FNP; ++k) roff[k] = ((fr0 + k * FRSTEP) * BN + fcc * 4) * 4;
+    f32x4 sum[FNP];
+#pragma unroll
+    for (int k = 0; k < FNP; ++k) sum[k] = __builtin_bit_cast(f32x4, raw_buffer_load_v4(rs, roff[k], 0, SC1));
+#pragma unroll 2
+    for (int q = 1; q < ksplit; ++q) {
+      f32x4 a[FNP];
+#pragma unroll
+      for (int k = 0; k < FNP; ++k) a[k] = __builtin_bit_cast(f32x4, raw_buffer_load_v4(rs, roff[k] + q * (TILE_F * 4), 0, SC1));
+#pragma unroll
+      for (int k = 0; k < FNP; ++k) sum[k] += a[k];
     }
     // back through the staging tile so the stores keep the OutT chunking of the plain path
     __syncthreads();

@@ -318,8 +318,11 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_LAT_UNITS") lat_units = v;
     else if (k == "TV_LAT_SPLIT") lat_split_max = std::max(1, std::min(8, v));
     else if (k == "TV_LAT_SPLIT_MIN") lat_split_min_nks = std::max(0, v);
+    else if (k == "TV_LAT_F32") lat_f32 = v ? 1 : 0;
+    else if (k == "TV_LAT_SPLIT_F32") lat_split_max_f32 = std::max(1, std::min(16, v));
     else if (k == "TV_PIPE_SPLIT") pipe_split_mode = std::max(0, std::min(2, v));
     else if (k == "TV_PIPE_SPLIT_MAX") pipe_split_max = std::max(1, std::min(64, v));
+    else if (k == "TV_PIPE_SPLIT_RED") pipe_split_red = std::max(0, v);
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
     else if (k == "TV_CT3") ct3_mode = v ? 1 : 0;
     else if (k == "TV_BURST") burst_mode = std::max(0, std::min(2, v));
@@ -957,7 +960,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   // levels: a few 512-pixel tiles on 256 CUs) -> conv_lat.hip (small tiles, K split over waves)
   ws->lat.assign(plan.ops.size(), 0);
   const int lat_min = lat_units >= 0 ? lat_units : cu_count;
-  for (size_t i = 0; lat_mode && dtype != F32 && i < plan.ops.size(); ++i) {
+  for (size_t i = 0; lat_mode && (dtype != F32 || lat_f32) && i < plan.ops.size(); ++i) {
     const OpSpec& op = plan.ops[i];
     ConvParams& p = ws->params[i];
     if (op.kind != OP_CONV || op.up_s || op.out < 0 || op.add >= 0 || (int)i == stem_op || (int)i == ss2_op ||
@@ -996,7 +999,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
   // no k-step chain, no split-K hand-off (knob TV_BURST=0 keeps them on conv_lat)
   ws->burst.assign(plan.ops.size(), 0);
   ws->bparams.assign(plan.ops.size(), BurstParams{});
-  for (size_t i = 0; burst_mode && i < plan.ops.size(); ++i) {
+  for (size_t i = 0; burst_mode && dtype != F32 && i < plan.ops.size(); ++i) {  // (fp16 / bf16 kernel)
     if (!ws->lat[i]) continue;
     BurstParams bp{};
     if (!conv_burst_plan(ws->params[i], B, &bp)) continue;
@@ -1053,7 +1056,10 @@ int Engine::make_workspace(int B, Workspace* ws) {
       // (write-through partial tiles, ticket, sc1 loads) costs more than it saves on the 18-20 k-step
       // 128-channel layers (R18 1.295 -> 1.269 ms without it) and far less on DLA-34's 36-72 k-step
       // 256 / 512-channel ones (1.284 -> 1.398 ms without it)
-      int ks = p.nks >= lat_split_min_nks ? std::min(lat_split_max, p.nks / 2) : 1;
+      // (fp32: a k-step is a quarter of the fp16 one's MFMA rate at half its depth, so the chains are
+      // twice as long and 2x slower per step: up to lat_split_max_f32 slices)
+      const int smax = dtype == F32 ? lat_split_max_f32 : lat_split_max;
+      int ks = p.nks >= lat_split_min_nks ? std::min(smax, p.nks / 2) : 1;
       ks = std::min(ks, cu_count / std::max(1, tiles));
       p.ksplit = ks > 1 ? ks : 0;
       if (!p.ksplit) continue;
@@ -1127,11 +1133,11 @@ int Engine::make_workspace(int B, Workspace* ws) {
       TV_HIP(hipDeviceSynchronize());
     }
   }
-  // conv_pipe split-K (MODE 0) for layers whose 256 x 128 tiles fill a fraction of the CUs: the fp32
-  // path's deep levels at small batches (R18 at B=1: 15x20 / 512-channel 3x3, 2 x 4 tiles of 144
-  // k-steps on 8 of 256 CUs). ksplit workgroups per tile, each slice >= 4 k-steps (the ring depth
-  // plus one), tiles x slices within one round of CUs; partial tiles meet in pslab, tickets in pcnt
-  // (knob TV_PIPE_SPLIT: 0 off, 1 fp32 only, 2 every dtype; TV_PIPE_SPLIT_MAX slices per tile)
+  // conv_pipe split-K (MODE 0) for layers whose 256 x 128 tiles fill the CUs badly: the fp32 path's
+  // deep levels at small batches (R18 at B=1: a 15x20 level is 2 tiles of 36 k-steps on 2 of 256
+  // CUs) and its 300-tile 240x320 layers (two rounds, the second 17% full). ksplit workgroups per
+  // tile, partial tiles meet in pslab, tickets in pcnt (knob TV_PIPE_SPLIT: 0 off, 1 fp32 only,
+  // 2 every dtype; TV_PIPE_SPLIT_MAX slices per tile; TV_PIPE_SPLIT_RED hand-off cost)
   {
     size_t slab_floats = 0, tickets = 0;
     for (size_t i = 0; i < nops; ++i) {
@@ -1139,8 +1145,18 @@ int Engine::make_workspace(int B, Workspace* ws) {
       const OpSpec& op = plan.ops[i];
       if (!ws->use_pipe[i] || op.kind == OP_CONVT_ADD || op.up_s) continue;
       if (!(pipe_split_mode == 2 || (pipe_split_mode == 1 && dtype == F32))) continue;
-      const int tiles = p.mtiles * p.ntiles;
-      int ks = std::min({pipe_split_max, cu_count / std::max(1, tiles), p.nks / 4});
+      // slices per tile by a cost model in tenths of a k-step: rounds of workgroups x k-steps per
+      // slice, plus the hand-off (each slice's partial tile written, then read by the reducer:
+      // pipe_split_red per slice); split only when it saves >= 10%
+      const long tiles = (long)p.mtiles * p.ntiles;
+      auto cost = [&](int k) {
+        const long rounds = (tiles * k + cu_count - 1) / cu_count;
+        return rounds * ((p.nks + k - 1) / k) * 10 + (k > 1 ? (long)pipe_split_red * (k + 1) : 0);
+      };
+      int ks = 1;
+      for (int k = 2; k <= pipe_split_max && k <= p.nks / 2; ++k)
+        if (cost(k) < cost(ks)) ks = k;
+      if (cost(ks) * 10 > cost(1) * 9) ks = 1;
       p.ksplit = ks > 1 ? ks : 0;
       if (!p.ksplit) continue;
       slab_floats = std::max(slab_floats, (size_t)tiles * ks * kPipeTileM * 128);

@@ -111,6 +111,9 @@ struct Engine {
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)
   int pipe_split_mode = 1;     // conv_pipe split-K on under-filled layers: 0 off, 1 fp32 only, 2 every dtype (TV_PIPE_SPLIT)
   int pipe_split_max = 16;     // ... at most this many slices per tile (knob TV_PIPE_SPLIT_MAX)
+  int pipe_split_red = 5;      // ... hand-off cost per slice in tenths of a k-step (knob TV_PIPE_SPLIT_RED)
+  int lat_f32 = 1;             // conv_lat.hip on the fp32 path too (knob TV_LAT_F32=0 off)
+  int lat_split_max_f32 = 8;   // ... its split-K cap there (knob TV_LAT_SPLIT_F32)
   int lat_split_min_nks = 32;  // ... for layers of at least this many k-steps (knob TV_LAT_SPLIT_MIN)
   int stamp_op = -1;           // diagnostics: op whose conv3x3 launch gets a stamp buffer (knob TV_C3_STAMPS=op:ptr)
   unsigned long long* stamp_buf = nullptr;

@@ -67,9 +67,9 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): LDS-DMA base in M0
 
-  // split-K (MODE 0, ksplit > 1): ksplit workgroups per tile, adjacent in the XCD-contiguous order
+  // split-K (ksplit > 1; either epilogue): ksplit workgroups per tile, adjacent in the XCD-contiguous order
   // so a tile's slices tend to share an L2; slice s walks k-steps [ks0, ks1)
-  const int ksplit = MODE == 0 && p.ksplit > 1 ? p.ksplit : 1;
+  const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
   const int nb = p.mtiles * p.ntiles * ksplit;
   const int bid = blockIdx.x;
   const int q8 = nb >> 3, r8 = nb & 7, xcd = bid & 7;
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   const int cc = tid % CPR;
   const int r0 = tid / CPR;
   const int n = n0 + cc * OVEC;
-  if (MODE == 0 && split) {
+  if (split) {
     // Split-K hand-off (the conv_lat.hip scheme): the partial tile goes to slab[tile][slice] with
     // write-through sc1 stores, each wave drains them, the workgroup barrier orders that before one
     // relaxed agent-scope ticket; the workgroup drawing ksplit - 1 sums the slices in slice order
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     f32x4 sum[FNP];
 #pragma unroll
     for (int k = 0; k < FNP; ++k) sum[k] = __builtin_bit_cast(f32x4, raw_buffer_load_v4(rs, roff[k], 0, SC1));
-#pragma unroll 2
+#pragma unroll 1
     for (int q = 1; q < ksplit; ++q) {
       f32x4 a[FNP];
 #pragma unroll
@@ -432,7 +432,7 @@ template <typename T, typename OutT, int MODE>
 static int launch_pipe_t(const ConvParams& p, const ConvParams* dp, void* out, hipStream_t s) {
   auto k = conv_pipe<T, OutT, MODE>;
   if (int r = ensure_lds<conv_pipe<T, OutT, MODE>>(LDS)) return r;
-  const int ksplit = MODE == 0 && p.ksplit > 1 ? p.ksplit : 1;
+  const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
   if (ksplit > 1 && (!p.slab || !p.cnt || ksplit > p.nks)) return 1;  // TV_EINVAL
   hipLaunchKernelGGL(k, dim3(p.mtiles * p.ntiles * ksplit), dim3(NT), LDS, s, dp, out);
   TV_HIP(hipGetLastError());

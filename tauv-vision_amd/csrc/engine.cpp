@@ -1133,7 +1133,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
       TV_HIP(hipDeviceSynchronize());
     }
   }
-  // conv_pipe split-K (MODE 0) for layers whose 256 x 128 tiles fill the CUs badly: the fp32 path's
+  // conv_pipe split-K for layers whose 256 x 128 tiles fill the CUs badly: the fp32 path's
   // deep levels at small batches (R18 at B=1: a 15x20 level is 2 tiles of 36 k-steps on 2 of 256
   // CUs) and its 300-tile 240x320 layers (two rounds, the second 17% full). ksplit workgroups per
   // tile, partial tiles meet in pslab, tickets in pcnt (knob TV_PIPE_SPLIT: 0 off, 1 fp32 only,
@@ -1142,8 +1142,7 @@ int Engine::make_workspace(int B, Workspace* ws) {
     size_t slab_floats = 0, tickets = 0;
     for (size_t i = 0; i < nops; ++i) {
       ConvParams& p = ws->params[i];
-      const OpSpec& op = plan.ops[i];
-      if (!ws->use_pipe[i] || op.kind == OP_CONVT_ADD || op.up_s) continue;
+      if (!ws->use_pipe[i]) continue;  // (both epilogues: the ConvT phase scatter + add runs after the sum)
       if (!(pipe_split_mode == 2 || (pipe_split_mode == 1 && dtype == F32))) continue;
       // slices per tile by a cost model in tenths of a k-step: rounds of workgroups x k-steps per
       // slice, plus the hand-off (each slice's partial tile written, then read by the reducer:

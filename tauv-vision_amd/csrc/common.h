@@ -215,7 +215,8 @@ struct DcnParams {
 };
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad);
 // dcn64_mode: 0 dcn_gemm; 1 64-channel k-steps when C % 64 == 0 (dcn_gemm64); 2 the same on 64-pixel
-// tiles; 3 the LDS-window kernel (dcn_win) where dcn_win_supported, else as 1
+// tiles; 3 the LDS-window kernel (dcn_win) where dcn_win_supported, else as 1; 5 dcn_gemm64d (gathers two
+// k-steps ahead, 64-pixel tiles) when C % 64 == 0 and om_ldc is even
 int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, int cu_count, hipStream_t s);
 bool dcn_win_supported(const DcnParams& p);
 // targets.hip: training targets of the loss (loss.py:31-135)

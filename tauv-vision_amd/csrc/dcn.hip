@@ -495,6 +495,243 @@ __global__ __launch_bounds__(NT, (min_blocks2<BN, PX>())) void dcn_gemm64(const 
     }
 }
 
+// ---- dcn_gemm64 with the corner gathers two k-steps ahead (knob TV_DCN64=5, round 6). PMC on the
+// B=32 DLA-34 forward (SQ_WAIT_ANY / SQ_WAVE_CYCLES): dcn_gemm64<64, 64>'s waves are parked on
+// s_waitcnt / the k-step barrier 57% of their cycles, VALU 14%, MFMA 9% busy: each wave waits every
+// k-step for the corner rows it requested one k-step earlier, and one k-step of blend + MFMA work
+// (x 4 waves per SIMD) is shorter than an L2 / MALL gather round trip. Here every thread owns two
+// operand sets (corners, blend weights, weight chunks) and step s + 2's gathers are issued right
+// after step s's blend freed its set, so a gather has two k-steps of the SIMD's work to land in.
+// Every global load of the main loop is unconditional (clamped step, OOB offsets) so the compiler's
+// counted waits stay exact; the per-(pixel, tap) sampling state is computed three taps ahead into a
+// 4-slot LDS ring from offset / mask values loaded one k-step before they are needed. Same
+// expressions, blend arithmetic, K order and MFMA sequence as dcn_gemm64: identical results.
+template <int BN, int PX> constexpr int lds_bytes2d() { return 2 * (abuf2<PX>() + wbuf2<BN>()) + 4 * pslot<PX>(); }
+template <int BN, int PX> constexpr int min_blocks2d() {
+  return 160 * 1024 / lds_bytes2d<BN, PX>() < 3 ? 160 * 1024 / lds_bytes2d<BN, PX>() : 3;
+}
+__device__ unsigned raw_buffer_load_u32(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.i32");
+template <typename T>
+__device__ __forceinline__ float half_of(unsigned v, int hi) {
+  const uint16_t b = (uint16_t)(hi ? v >> 16 : v & 0xffffu);
+  return (float)__builtin_bit_cast(T, b);
+}
+
+template <typename T, int BN, int PX>
+__global__ __launch_bounds__(NT, (min_blocks2d<BN, PX>())) void dcn_gemm64d(const DcnParams p) {
+  constexpr int PJ = PX / 32;
+  constexpr int WPX = PX / 32;
+  constexpr int NA = BN / 32 / (4 / WPX);
+  constexpr int WBUF = wbuf2<BN>();
+  constexpr int ABUF2 = abuf2<PX>();
+  constexpr int PSLOT = pslot<PX>();
+  constexpr int WCH = BN * 8 / NT;
+  constexpr int RSL = 4;  // sampling-state ring slots
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const Pring = smem + 2 * (ABUF2 + WBUF);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, lh = lane >> 5;
+  const int HW = p.H * p.W;
+  const int M = p.B * HW;
+  const int G = gridDim.x, ny = p.N / BN;
+  const int q = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int m0 = (q / ny) * PX, n0 = (q % ny) * BN;
+  const int ncb = p.C / 64;
+  const int S = 9 * ncb;
+
+  i32x4 xr, wrs, omr;
+  {
+    const unsigned long long a = (unsigned long long)p.x, aw = (unsigned long long)p.w, ao = (unsigned long long)p.om;
+    xr = i32x4{(int)(unsigned)a, (int)(unsigned)(a >> 32), (int)((unsigned)M * p.ldx * (unsigned)sizeof(T)), 0x00020000};
+    wrs = i32x4{(int)(unsigned)aw, (int)(unsigned)(aw >> 32), (int)((unsigned)p.N * p.Kpad * (unsigned)sizeof(T)),
+                0x00020000};
+    omr = i32x4{(int)(unsigned)ao, (int)(unsigned)(ao >> 32), (int)((unsigned)M * p.om_ldc * (unsigned)sizeof(T)),
+                0x00020000};
+  }
+
+  // ---- sampling-state producer: thread tid < PX owns pixel tid (dcn_sample's expressions)
+  const int pm = m0 + (tid & (PX - 1));
+  const bool pval = tid < PX && pm < M;
+  const int pb = pval ? pm / HW : 0;
+  const int prem = pval ? pm - pb * HW : 0;
+  const int poy = prem / p.W, pox = prem - (prem / p.W) * p.W;
+  const int ombase = pval ? pm * p.om_ldc * (int)sizeof(T) : kOOB;  // (om_ldc even: 4-byte aligned pairs)
+  // om values of tap k: the (dy, dx) pair and the dword holding the mask logit (half k & 1)
+  auto om_load = [&](int k, unsigned& dydx, unsigned& lg) __attribute__((always_inline)) {
+    dydx = raw_buffer_load_u32(omr, ombase + 4 * k, 0, 0);
+    lg = raw_buffer_load_u32(omr, ombase + 36 + 4 * (k >> 1), 0, 0);
+  };
+  auto tap_state = [&](int k, unsigned dydx, unsigned lg, bool write) __attribute__((always_inline)) {
+    int vo[4] = {kOOB, kOOB, kOOB, kOOB};
+    float wt[4] = {0.f, 0.f, 0.f, 0.f};
+    const float dy = half_of<T>(dydx, 0), dx = half_of<T>(dydx, 1), logit = half_of<T>(lg, k & 1);
+    if (pval) {
+      const float mask = 1.0f / (1.0f + expf(-logit));
+      const float py = (float)(poy - 1 + k / 3) + dy;
+      const float px = (float)(pox - 1 + k % 3) + dx;
+      if (py > -1.f && py < (float)p.H && px > -1.f && px < (float)p.W) {
+        const float fy = floorf(py), fx = floorf(px);
+        const int y0 = (int)fy, x0 = (int)fx;
+        const float ly = py - fy, lx = px - fx, hy = 1.f - ly, hx = 1.f - lx;
+        const float w4[4] = {hy * hx, hy * lx, ly * hx, ly * lx};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int yy = y0 + (c >> 1), xx = x0 + (c & 1);
+          if (yy >= 0 && yy <= p.H - 1 && xx >= 0 && xx <= p.W - 1) {
+            vo[c] = ((pb * HW + yy * p.W + xx) * p.ldx) * (int)sizeof(T);
+            wt[c] = w4[c] * mask;
+          }
+        }
+      }
+    }
+    if (write && tid < PX) {
+      int* d = reinterpret_cast<int*>(Pring + (k % RSL) * PSLOT + tid * 32);
+      *reinterpret_cast<int4*>(d) = make_int4(vo[0], vo[1], vo[2], vo[3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(wt[0], wt[1], wt[2], wt[3]);
+    }
+  };
+
+  // ---- operand sets: corners, blend weights and weight chunks of one k-step
+  const int gc = tid & 7, gg = tid >> 3;
+  struct Set {
+    uint4 cv[PJ][4];
+    float wts[PJ][4];
+    uint4 wv[WCH];
+  };
+  Set A, B;
+  // step s's operands into set X: its tap's state from the ring (offsets -> gathers, weights kept)
+  auto prepare = [&](int s, Set& X) __attribute__((always_inline)) {
+    const int k = s / ncb, cb = s - k * ncb;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      const int* d = reinterpret_cast<const int*>(Pring + (k % RSL) * PSLOT + (gg + 32 * j) * 32);
+      const int4 o = *reinterpret_cast<const int4*>(d);
+      const float4 w = *reinterpret_cast<const float4*>(d + 4);
+      const int vo[4] = {o.x, o.y, o.z, o.w};
+      X.wts[j][0] = w.x; X.wts[j][1] = w.y; X.wts[j][2] = w.z; X.wts[j][3] = w.w;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) X.cv[j][c] = to_u4(raw_buffer_load_v4(xr, vo[c] + 16 * gc, cb * 64 * (int)sizeof(T), 0));
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) {
+      const int r = (tid + NT * i) >> 3;
+      X.wv[i] = to_u4(raw_buffer_load_v4(wrs, ((n0 + r) * p.Kpad + 8 * gc) * (int)sizeof(T), s * 64 * (int)sizeof(T), 0));
+    }
+  };
+  auto produce = [&](int s, const Set& X) __attribute__((always_inline)) {
+    char* Ab = smem + (s & 1) * (ABUF2 + WBUF);
+    char* Wl = Ab + ABUF2;
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+      unsigned o[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        float a0, a1;
+        if constexpr (std::is_same<T, _Float16>::value) {
+          const unsigned d0 = reinterpret_cast<const unsigned*>(&X.cv[j][0])[e >> 1];
+          a0 = mix_lo(X.wts[j][0], d0);
+          a1 = mix_hi(X.wts[j][0], d0);
+#pragma unroll
+          for (int c = 1; c < 4; ++c) {
+            const unsigned dw = reinterpret_cast<const unsigned*>(&X.cv[j][c])[e >> 1];
+            a0 = mix_lo_acc(X.wts[j][c], dw, a0);
+            a1 = mix_hi_acc(X.wts[j][c], dw, a1);
+          }
+        } else {
+          a0 = 0.f;
+          a1 = 0.f;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            a0 += X.wts[j][c] * elem<T>(X.cv[j][c], e);
+            a1 += X.wts[j][c] * elem<T>(X.cv[j][c], e + 1);
+          }
+        }
+        o[e >> 1] = pack2<T>(a0, a1);
+      }
+      *reinterpret_cast<uint4*>(Ab + sw2(gg + 32 * j, gc)) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < WCH; ++i) *reinterpret_cast<uint4*>(Wl + sw2((tid + NT * i) >> 3, gc)) = X.wv[i];
+  };
+
+  f32x16 acc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) acc[i] = f32x16{};
+  const int wp = wave % WPX, wc = wave / WPX;
+  auto consume = [&](int s) __attribute__((always_inline)) {
+    const char* Ab = smem + (s & 1) * (ABUF2 + WBUF);
+    const char* Wl = Ab + ABUF2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint4 xf = *reinterpret_cast<const uint4*>(Ab + sw2(32 * wp + l32, 2 * j + lh));
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const uint4 wf = *reinterpret_cast<const uint4*>(Wl + sw2(32 * (wc * NA + i) + l32, 2 * j + lh));
+        Mfma<T>::run(wf, xf, acc[i]);
+      }
+    }
+  };
+
+  // ---- prologue: the states of taps 0..2, the om values for the loop's first state (tap 3), the
+  // operands of steps 0 and 1
+  {
+    unsigned d0, l0, d1, l1, d2, l2;
+    om_load(0, d0, l0);
+    om_load(1, d1, l1);
+    om_load(2, d2, l2);
+    tap_state(0, d0, l0, true);
+    tap_state(1, d1, l1, true);
+    tap_state(2, d2, l2, true);
+  }
+  unsigned om_dydx, om_lg;  // om values for the state computed in the next iteration
+  om_load(3, om_dydx, om_lg);
+  __syncthreads();
+  prepare(0, A);
+  prepare(min(1, S - 1), B);
+  // iteration s: blend step s (its set then free), the tap-(k+3) state when s starts tap k, the
+  // om values of the next iteration's state, step s + 2's operands into the freed set (past the
+  // end: the last step again, unused), barrier, step s's MFMAs
+  auto iter = [&](int s, Set& X) __attribute__((always_inline)) {
+    const int k = s / ncb, cb = s - k * ncb;
+    produce(s, X);
+    const int tk = min(k + 3, 8);
+    tap_state(tk, om_dydx, om_lg, cb == 0 && k + 3 < 9);
+    const int s1 = s + 1;
+    const int k1n = min(min(s1, S - 1) / ncb + 3, 8);
+    om_load(k1n, om_dydx, om_lg);
+    prepare(min(s + 2, S - 1), X);
+    __syncthreads();
+    consume(s);
+  };
+  for (int s = 0;;) {
+    iter(s, A);
+    if (++s == S) break;
+    iter(s, B);
+    if (++s == S) break;
+  }
+
+  // ---- epilogue (as dcn_gemm64)
+  const int mo = m0 + 32 * wp + l32;
+  if (mo >= M) return;
+  T* dst = reinterpret_cast<T*>(p.out) + (size_t)mo * p.out_ldc + n0;
+#pragma unroll
+  for (int i = 0; i < NA; ++i)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int ch = 32 * (wc * NA + i) + 8 * g + 4 * lh;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = acc[i][4 * g + e] + p.bias[n0 + ch + e];
+        if (p.act == 1) t = fmaxf(t, 0.0f);
+        else if (p.act == 2) t = fmaxf(t, 0.01f * t);
+        v[e] = t;
+      }
+      typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2*>(dst + ch) = u32x2{pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3])};
+    }
+}
+
 // ---- window variant (C == N == 64: DLA-34's 120x160 DeformConvs, node_k of ida_2 / ida_up, two
 // thirds of its DCN time). dcn_gemm64 gathers every corner from L1/L2: 9 taps x 4 corners x 128 B
 // per pixel, ~15 TB/s of useful bytes, the TA/TD rate of 16-byte gathers (MI355X_MICROARCH.md,
@@ -820,6 +1057,15 @@ static void launch_win(const DcnParams& p, int cu_count, hipStream_t s) {
 }
 
 template <typename T, int BN, int PX>
+static void launch64d(const DcnParams& p, hipStream_t s) {
+  constexpr int lds = lds_bytes2d<BN, PX>();
+  (void)ensure_lds<dcn_gemm64d<T, BN, PX>>(lds);
+  const long M = (long)p.B * p.H * p.W;
+  const dim3 grid((unsigned)((M + PX - 1) / PX * (p.N / BN)));
+  hipLaunchKernelGGL((dcn_gemm64d<T, BN, PX>), grid, dim3(NT), lds, s, p);
+}
+
+template <typename T, int BN, int PX>
 static void launch64(const DcnParams& p, hipStream_t s) {
   constexpr int lds = lds_bytes2<BN, PX>();
   (void)ensure_lds<dcn_gemm64<T, BN, PX>>(lds);
@@ -855,7 +1101,7 @@ int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, int cu_count,
     set_error("dcn_gemm: fp16/bf16 only");
     return 1;
   }
-  if (dcn64_mode >= 3 && dcn_win_supported(p)) {  // LDS window (C == N == 64; mode 4: diagnostics only)
+  if ((dcn64_mode == 3 || dcn64_mode == 4) && dcn_win_supported(p)) {  // LDS window (C == N == 64; mode 4: diagnostics only)
     if (dtype == F16) dcn::launch_win<_Float16>(p, cu_count, s);
     else dcn::launch_win<__bf16>(p, cu_count, s);
   } else if (p.C % 64 == 0 && dcn64_mode) {  // full-line gathers (every DLA-34 DeformConv); mode 2: 64-pixel tiles
@@ -864,7 +1110,15 @@ int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, int cu_count,
     // too when 128-pixel tiles would leave few workgroups per CU (B=1: 1.65 -> 1.52 ms; B=64 neutral)
     const long tiles128 = (M + 127) / 128 * (p.N / 128);
     const bool px64w = dcn64_mode == 2 || tiles128 < 1024;
-    if (dtype == F16) {
+    if (dcn64_mode == 5 && p.om_ldc % 2 == 0) {  // gathers two k-steps ahead (64-pixel tiles)
+      if (dtype == F16) {
+        if (wide) dcn::launch64d<_Float16, 128, 64>(p, s);
+        else dcn::launch64d<_Float16, 64, 64>(p, s);
+      } else {
+        if (wide) dcn::launch64d<__bf16, 128, 64>(p, s);
+        else dcn::launch64d<__bf16, 64, 64>(p, s);
+      }
+    } else if (dtype == F16) {
       if (wide) px64w ? dcn::launch64<_Float16, 128, 64>(p, s) : dcn::launch64<_Float16, 128, 128>(p, s);
       else dcn::launch64<_Float16, 64, 64>(p, s);
     } else {

@@ -46,11 +46,11 @@ namespace tv {
 // centerpoint_dla.py:389-391; 3x3, stride 1, pad 1) + bias + activation, as the engine runs it:
 // variant 0 = fused dcn_gemm (32-channel k-steps), 1 = fused dcn_gemm64 (tile by size),
 // 2 = dcn_gemm64 with 64-pixel tiles, 3 = unfused (dcn_sample column tensor + implicit GEMM: the
-// fp32 path). weight: host fp32 [N][C][3][3] (PyTorch layout), K packed tap-major as the engine does.
+// fp32 path), 4 = dcn_win (C == N == 64), 5 = dcn_gemm64d (gathers two k-steps ahead). weight: host fp32 [N][C][3][3] (PyTorch layout), K packed tap-major as the engine does.
 int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int om_ldc, const float* weight,
                   const float* bias, int N, int act, int dtype, int variant, void* out, hipStream_t s) {
   if (!x || !om || !weight || !bias || !out || B < 1 || H < 1 || W < 1 || C < 1 || N < 1 || om_ldc < 27 ||
-      variant < 0 || variant > 4 || dtype < F32 || dtype > BF16 || act < 0 || act > 2) {
+      variant < 0 || variant > 5 || dtype < F32 || dtype > BF16 || act < 0 || act > 2) {
     set_error("diag_dcn_conv: bad argument");
     return TV_EINVAL;
   }
@@ -76,7 +76,7 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
   TV_HIP(hipMalloc(&db.p, hb.size() * 4));
   TV_HIP(hipMemcpy(db.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
   int rc = 0;
-  if (variant < 3 || variant == 4) {
+  if (variant != 3) {
     DcnParams q{};
     q.x = x;
     q.B = B;

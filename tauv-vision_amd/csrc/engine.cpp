@@ -1519,8 +1519,10 @@ const char* Engine::op_kernel(int B, size_t i) {
       else if (ws->dcn[i].x) {
         const DcnParams& d = ws->dcn[i];
         const bool wide = d.N % 128 == 0;
-        if (dcn64_mode >= 3 && dcn_win_supported(d)) {
+        if ((dcn64_mode == 3 || dcn64_mode == 4) && dcn_win_supported(d)) {
           name = std::string("tv::dcn::dcn_win<") + t + ">";
+        } else if (dcn64_mode == 5 && d.C % 64 == 0 && d.om_ldc % 2 == 0) {
+          name = std::string("tv::dcn::dcn_gemm64d<") + t + (wide ? ", 128, 64>" : ", 64, 64>");
         } else if (dcn64_mode && d.C % 64 == 0) {  // dcn_gemm64<T, BN, PX>: the pixel tile as launch_dcn_gemm picks it
           const long tiles128 = ((long)d.B * d.H * d.W + 127) / 128 * (d.N / 128);
           const int px = !wide || dcn64_mode == 2 || tiles128 < 1024 ? 64 : 128;

@@ -100,7 +100,8 @@ struct Engine {
                                // (env TV_LAT=0 off)
   int dcn64_mode = 1;          // fused DCN with 64-channel k-steps (full-line gathers) when C % 64 == 0 (knob TV_DCN64:
                                // 0 dcn_gemm, 2 dcn_gemm64 on 64-pixel tiles, 3 the LDS-window dcn_win for C == N == 64:
-                               // bit-equal, measured 194 vs 187 us per 120x160 layer, so not the default)
+                               // bit-equal, measured 194 vs 187 us per 120x160 layer, so not the default; 5 dcn_gemm64d:
+                               // the corner gathers two k-steps ahead)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
   int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1; 2 = N <= 128 only)
   int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)

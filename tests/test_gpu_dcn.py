@@ -37,7 +37,7 @@ TOL = {"fp32": 2e-5, "fp16": 4e-3, "bf16": 3e-2}
 def variants(precision, C, N=None):
     if precision == "fp32":
         return [3]
-    v = [0, 1, 2, 3] if C % 64 == 0 else [0, 3]
+    v = [0, 1, 2, 3, 5] if C % 64 == 0 else [0, 3]
     return v + [4] if C == 64 and N == 64 else v
 
 
@@ -97,9 +97,9 @@ def test_dcn_zero_offsets_unit_mask_is_conv(precision, shape):
     outs = {v: dcn_gpu(x, om, w, b, 0, precision, v) for v in variants(precision, C, N)}
     for v, o in outs.items():
         assert_close(o, ref, ULP[precision], f"variant {v}")
-    fused = [o for v, o in outs.items() if v in (0, 1, 2, 4)]
+    fused = [o for v, o in outs.items() if v in (0, 1, 2, 4, 5)]
     for o in fused[1:]:
-        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 / dcn_win tilings must be bit-identical"
+        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 / dcn_win / dcn_gemm64d tilings must be bit-identical"
 
 
 def shifted_conv(x, w, b, dy, dx):
@@ -160,9 +160,9 @@ def test_dcn_bilinear_vs_oracle_restatement(precision, shape):
     outs = {v: dcn_gpu(x, om, w, b, 1, precision, v) for v in variants(precision, C, N)}
     for v, o in outs.items():
         assert_close(o, ref.clamp_min(0.0), TOL[precision], f"variant {v}")
-    fused = [o for v, o in outs.items() if v in (0, 1, 2, 4)]
+    fused = [o for v, o in outs.items() if v in (0, 1, 2, 4, 5)]
     for o in fused[1:]:
-        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 / dcn_win tilings must be bit-identical"
+        assert torch.equal(o, fused[0]), "dcn_gemm / dcn_gemm64 / dcn_win / dcn_gemm64d tilings must be bit-identical"
 
 
 @pytest.mark.parametrize("precision", ["fp16", "bf16"])
@@ -181,3 +181,17 @@ def test_dcn_window_kernel_multi_tile_bit_equal(precision, sigma):
     off, logit = om[:, :18], om[:, 18:]
     ref = deform_conv2d(x.double(), off.double(), torch.sigmoid(logit.double()), w.double(), b.double()).float()
     assert_close(got, ref.clamp_min(0.0), TOL[precision], "dcn_win")
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("shape", [(3, 64, 37, 45, 64), (2, 128, 30, 41, 128), (1, 256, 15, 20, 128), (4, 64, 60, 80, 64)])
+def test_dcn_deep_prefetch_bit_equal(precision, shape):
+    """dcn_gemm64d (variant 5: gathers two k-steps ahead, sampling state three taps ahead in a
+    4-slot ring, every main-loop load unconditional) over many workgroups, odd step counts (9 k-steps
+    at C = 64) and 2 / 4 channel blocks per tap: bit-equal to dcn_gemm64 on 64-pixel tiles."""
+    B, C, H, W, N = shape
+    x, w, b, g = inputs(B, C, H, W, N, precision, 23)
+    om = rnd(om_of(torch.randn(B, 9, H, W, generator=g) * 1.5, torch.randn(B, 9, H, W, generator=g) * 1.5,
+                   torch.randn(B, 9, H, W, generator=g) * 2.0), precision)
+    got = dcn_gpu(x, om, w, b, 1, precision, 5)
+    assert torch.equal(got, dcn_gpu(x, om, w, b, 1, precision, 2)), "dcn_gemm64d must equal dcn_gemm64 bit for bit"

@@ -121,6 +121,22 @@ int tv_engine_profile(tv_engine* engine, const float* img_nchw, int32_t batch, f
 /* The same over raw u8 frames (the tv_engine_forward_u8 path). */
 int tv_engine_profile_u8(tv_engine* engine, const uint8_t* frames_nhwc, int32_t batch, float* out_nhwc,
                          void* stream, float* ms, double* flops, int32_t cap, int32_t* n_ops);
+/* Diagnostic: one forward_u8 exactly as it runs (concurrent slices, grouped launches) with a HIP
+ * event before each launch on its slice's stream (synchronous): ms[k * cap + i] = in-situ duration
+ * of op i's launch in slice k (a grouped launch's on its first op, 0 for the others), *n_slices
+ * slices (tv_engine_slices). The durations include waiting for CUs the other slices hold, which is
+ * what rocprofv3's kernel trace of the same run reports. */
+int tv_engine_forward_insitu_u8(tv_engine* engine, const uint8_t* frames_nhwc, int32_t batch, float* out_nhwc,
+                                void* stream, float* ms, int32_t cap, int32_t* n_slices);
+/* Diagnostic: while on, every forward records the group events tv_engine_forward_insitu uses, also
+ * into a graph captured meanwhile (event record nodes); tv_engine_insitu_read returns the times the
+ * B-frame forward on `stream` (its workspaces' key: the capture stream) last recorded, e.g. after
+ * a replay, in the ms[k * cap + i] layout above. */
+int tv_engine_set_insitu(tv_engine* engine, int32_t on);
+int tv_engine_insitu_read(tv_engine* engine, int32_t batch, void* stream, float* ms, int32_t cap, int32_t* n_slices);
+/* The same over the normalised fp32 NCHW input (the tv_engine_forward path). */
+int tv_engine_forward_insitu(tv_engine* engine, const float* img_nchw, int32_t batch, float* out_nhwc, void* stream,
+                             float* ms, int32_t cap, int32_t* n_slices);
 const char* tv_engine_op_label(tv_engine* engine, int32_t index);
 /* Kernel family launch `index` uses at this batch size ("conv_pipe", "conv_igemm", "conv_halo",
  * "prep"); "" before the batch's workspace exists. Diagnostic (roofline attribution). */

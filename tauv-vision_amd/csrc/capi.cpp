@@ -174,6 +174,46 @@ int tv_engine_profile_u8(tv_engine* e, const uint8_t* frames, int32_t B, float* 
   })
 }
 
+int tv_engine_set_insitu(tv_engine* e, int32_t on) {
+  TV_GUARD({
+    if (!e) { set_error("null engine"); return TV_EINVAL; }
+    e->e.insitu = on ? 1 : 0;
+    return TV_OK;
+  })
+}
+
+int tv_engine_insitu_read(tv_engine* e, int32_t B, void* stream, float* ms, int32_t cap, int32_t* n_slices) {
+  TV_GUARD({
+    if (!e || !ms || !n_slices || cap < 1 || B < 1) { set_error("bad argument"); return TV_EINVAL; }
+    int n = 0;
+    int rc = e->e.insitu_read(B, (hipStream_t)stream, ms, cap, &n);
+    *n_slices = n;
+    return rc;
+  })
+}
+
+int tv_engine_forward_insitu(tv_engine* e, const float* img, int32_t B, float* out, void* stream, float* ms,
+                             int32_t cap, int32_t* n_slices) {
+  TV_GUARD({
+    if (!e || !img || !out || !ms || !n_slices || cap < 1) { set_error("null argument"); return TV_EINVAL; }
+    int n = 0;
+    int rc = e->e.forward_insitu(img, 0, B, out, (hipStream_t)stream, ms, cap, &n);
+    *n_slices = n;
+    return rc;
+  })
+}
+
+int tv_engine_forward_insitu_u8(tv_engine* e, const uint8_t* frames, int32_t B, float* out, void* stream, float* ms,
+                                int32_t cap, int32_t* n_slices) {
+  TV_GUARD({
+    if (!e || !frames || !out || !ms || !n_slices || cap < 1) { set_error("null argument"); return TV_EINVAL; }
+    int n = 0;
+    int rc = e->e.forward_insitu(frames, 1, B, out, (hipStream_t)stream, ms, cap, &n);
+    *n_slices = n;
+    return rc;
+  })
+}
+
 const char* tv_engine_op_label(tv_engine* e, int32_t i) {
   if (!e || i < 0 || i >= (int)e->e.plan.ops.size()) return "";
   return e->e.plan.ops[i].label.c_str();

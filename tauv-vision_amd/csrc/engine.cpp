@@ -444,6 +444,7 @@ Engine::~Engine() {
     if (kv.second->dparams) (void)hipFree(kv.second->dparams);
     if (kv.second->dks) (void)hipFree(kv.second->dks);
     if (kv.second->slab) (void)hipFree(kv.second->slab);
+    for (hipEvent_t ev : kv.second->gev) (void)hipEventDestroy(ev);
     if (kv.second->pslab) (void)hipFree(kv.second->pslab);
     if (kv.second->pcnt) (void)hipFree(kv.second->pcnt);
     if (kv.second->cnt) (void)hipFree(kv.second->cnt);
@@ -1198,6 +1199,7 @@ int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
     if (ws->dparams) (void)hipFree(ws->dparams);
     if (ws->dks) (void)hipFree(ws->dks);
     if (ws->slab) (void)hipFree(ws->slab);
+    for (hipEvent_t ev : ws->gev) (void)hipEventDestroy(ev);
     if (ws->pslab) (void)hipFree(ws->pslab);
     if (ws->pcnt) (void)hipFree(ws->pcnt);
     if (ws->cnt) (void)hipFree(ws->cnt);
@@ -1218,6 +1220,7 @@ int Engine::trim() {
     if (kv.second->dparams) (void)hipFree(kv.second->dparams);
     if (kv.second->dks) (void)hipFree(kv.second->dks);
     if (kv.second->slab) (void)hipFree(kv.second->slab);
+    for (hipEvent_t ev : kv.second->gev) (void)hipEventDestroy(ev);
     if (kv.second->pslab) (void)hipFree(kv.second->pslab);
     if (kv.second->pcnt) (void)hipFree(kv.second->pcnt);
     if (kv.second->cnt) (void)hipFree(kv.second->cnt);
@@ -1384,7 +1387,15 @@ int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStrea
   // the replays after the first on this ROCm: aux.hip fill_zero16)
   const size_t nops = plan.ops.size();
   if (op0 == 0 && op1 >= nops) {  // the whole forward: the schedule's groups
+    if (insitu && ws->gev.size() != ws->groups.size() + 1) {
+      for (hipEvent_t e : ws->gev) (void)hipEventDestroy(e);
+      ws->gev.assign(ws->groups.size() + 1, nullptr);
+      for (hipEvent_t& e : ws->gev) TV_HIP(hipEventCreate(&e));
+    }
+    size_t gi = 0;
     for (const std::vector<int>& g : ws->groups) {
+      if (insitu) TV_HIP(hipEventRecord(ws->gev[gi], s));
+      ++gi;
       if (g.size() == 1) {
         rc = run_op((size_t)g[0], ws, input, input_u8, out, s);
       } else if (ws->burst[g[0]]) {
@@ -1406,6 +1417,7 @@ int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStrea
       }
       if (rc) return rc;
     }
+    if (insitu) TV_HIP(hipEventRecord(ws->gev[gi], s));
     return TV_OK;
   }
   for (size_t k = op0; k < nops && k < op1; ++k) {  // positions op0 .. op1 - 1 of the execution order
@@ -1476,6 +1488,51 @@ int Engine::forward(const void* input, int input_u8, int B, float* out, hipStrea
     return TV_OK;
   }
   return run_all(input, input_u8, B, out, s);
+}
+
+int Engine::forward_insitu(const void* input, int input_u8, int B, float* out, hipStream_t s, float* ms, int cap,
+                           int* n_slices) {
+  if (slice_lag) {
+    set_error("forward_insitu: not with a slice lag");
+    return TV_EINVAL;
+  }
+  profiled_u8 = input_u8;
+  const int prev = insitu;
+  insitu = 1;
+  int rc = forward(input, input_u8, B, out, s);
+  insitu = prev;
+  if (rc) return rc;
+  TV_HIP(hipStreamSynchronize(s));  // (the side slices are joined into s)
+  return insitu_read(B, s, ms, cap, n_slices);
+}
+
+int Engine::insitu_read(int B, hipStream_t s, float* ms, int cap, int* n_slices) {
+  int rc = 0;
+  const std::vector<int> sz = slice_sizes(B);
+  SideStreams* ss = nullptr;
+  if (sz.size() > 1) {
+    rc = get_side(s, (int)sz.size() - 1, &ss);
+    if (rc) return rc;
+  }
+  const size_t nops = plan.ops.size();
+  for (size_t k = 0; k < sz.size(); ++k) {
+    Workspace* ws = nullptr;
+    rc = get_workspace(sz[k], k ? ss->s[k - 1] : s, &ws);
+    if (rc) return rc;
+    if (ws->gev.size() != ws->groups.size() + 1) {
+      set_error("forward_insitu: no events recorded");
+      return TV_EINVAL;
+    }
+    for (size_t i = 0; i < nops && (int)i < cap; ++i) ms[k * cap + i] = 0.f;
+    for (size_t gi = 0; gi < ws->groups.size(); ++gi) {
+      float t = 0;
+      TV_HIP(hipEventElapsedTime(&t, ws->gev[gi], ws->gev[gi + 1]));
+      const int i = ws->groups[gi][0];
+      if (i < cap) ms[k * cap + i] = t;
+    }
+  }
+  *n_slices = (int)sz.size();
+  return TV_OK;
 }
 
 const char* Engine::op_kernel(int B, size_t i) {

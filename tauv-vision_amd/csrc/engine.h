@@ -67,6 +67,7 @@ struct Workspace {
   std::vector<std::vector<int>> groups;  // the schedule: conv_lat layers of one level in one launch, others alone
   size_t cnt_bytes = 0;
   std::vector<std::string> kname;   // per op: kernel instance name (diagnostics), filled lazily
+  std::vector<hipEvent_t> gev;      // forward_insitu(): one event before each schedule group + one after the last
 };
 
 struct Engine {
@@ -130,6 +131,7 @@ struct Engine {
   static constexpr int kMaxSlices = 8;  // == TV_MAX_SLICES (include/tauv_vision_amd.h)
   int slices = 2;
   int slice_min = 8;
+  int insitu = 0;     // forward_insitu() in progress: run_all records the group events
   int slice_lag = 0;  // diagnostics (knob TV_SLICE_LAG): slice 1 starts after slice 0's op `slice_lag`
   std::vector<int> slice_sizes_env;
   std::vector<int> slice_sizes(int B) const;
@@ -151,6 +153,14 @@ struct Engine {
   int trim();                         // free every cached workspace (no forward may be in flight)
   int forward(const void* input, int input_u8, int B, float* out, hipStream_t s);
   int profile(const void* input, int input_u8, int B, float* out, hipStream_t s, float* ms, double* flops, int cap, int* n_ops);
+  // the forward as it runs (concurrent slices, schedule groups) with an event before each launch on
+  // its slice's stream: ms[k * cap + i] = launch time of op i in slice k (a grouped launch's time on
+  // its first op), *n_slices slices, synchronous (diagnostic: in-situ per-launch durations)
+  int forward_insitu(const void* input, int input_u8, int B, float* out, hipStream_t s, float* ms, int cap,
+                     int* n_slices);
+  // the times the group events of the B-frame forward on s last recorded (an eager forward_insitu,
+  // or the replay of a graph captured while `insitu` was set)
+  int insitu_read(int B, hipStream_t s, float* ms, int cap, int* n_slices);
   const char* op_kernel(int B, size_t i);
 
  private:

@@ -45,6 +45,12 @@ EXPORTS = {
                            ctypes.POINTER(c_i32)], c_i32),
     "tv_engine_profile_u8": ([c_vp, c_vp, c_i32, c_vp, c_vp, ctypes.POINTER(c_f32), ctypes.POINTER(c_f64), c_i32,
                               ctypes.POINTER(c_i32)], c_i32),
+    "tv_engine_forward_insitu_u8": ([c_vp, c_vp, c_i32, c_vp, c_vp, ctypes.POINTER(c_f32), c_i32,
+                                     ctypes.POINTER(c_i32)], c_i32),
+    "tv_engine_forward_insitu": ([c_vp, c_vp, c_i32, c_vp, c_vp, ctypes.POINTER(c_f32), c_i32,
+                                  ctypes.POINTER(c_i32)], c_i32),
+    "tv_engine_set_insitu": ([c_vp, c_i32], c_i32),
+    "tv_engine_insitu_read": ([c_vp, c_i32, c_vp, ctypes.POINTER(c_f32), c_i32, ctypes.POINTER(c_i32)], c_i32),
     "tv_engine_op_label": ([c_vp, c_i32], ctypes.c_char_p),
     "tv_engine_op_kernel": ([c_vp, c_i32, c_i32], ctypes.c_char_p),
     "tv_engine_slices": ([c_vp, c_i32, ctypes.POINTER(c_i32), ctypes.POINTER(c_i32)], c_i32),

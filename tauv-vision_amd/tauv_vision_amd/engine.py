@@ -66,6 +66,11 @@ class NativeEngine:
         _lib.check(_lib.lib().tv_engine_slices(self._h, batch, ctypes.byref(n), sb), "slices")
         return [sb[i] for i in range(n.value)]
 
+    def op_kernels(self, batch, n):
+        """Kernel instance of each of the first n ops in a `batch`-frame workspace ("" before it exists)."""
+        L = _lib.lib()
+        return [L.tv_engine_op_kernel(self._h, batch, i).decode() for i in range(n)]
+
     def alloc_out(self, batch):
         oh, ow, oc = self.out_shape_per_frame
         return torch.empty((batch, oh, ow, oc), dtype=torch.float32, device=self.device)
@@ -97,6 +102,34 @@ class NativeEngine:
                                                    ctypes.c_void_p(out.data_ptr()), _lib.stream_of(self.device)),
                    "forward_u8")
         return out
+
+    def profile_insitu(self, frames, out=None, cap=1024):
+        """One forward as it runs (concurrent slices, grouped launches), an event before each launch
+        on its slice's stream: per slice, per op index the launch's ms (0 for ops that launch nothing
+        of their own). `frames`: uint8 NHWC (forward_u8) or the fp32 NCHW forward() input."""
+        B = frames.shape[0]
+        if out is None:
+            out = self.alloc_out(B)
+        ns = ctypes.c_int32()
+        ms = (ctypes.c_float * (cap * 8))()
+        L = _lib.lib()
+        fn = L.tv_engine_forward_insitu_u8 if frames.dtype == torch.uint8 else L.tv_engine_forward_insitu
+        _lib.check(fn(self._h, ctypes.c_void_p(frames.data_ptr()), B, ctypes.c_void_p(out.data_ptr()),
+                      _lib.stream_of(self.device), ms, cap, ctypes.byref(ns)), "forward_insitu")
+        return [[ms[k * cap + i] for i in range(cap)] for k in range(ns.value)]
+
+    def set_insitu(self, on):
+        """Record the per-launch group events in every forward (also into a graph captured meanwhile)."""
+        _lib.check(_lib.lib().tv_engine_set_insitu(self._h, 1 if on else 0), "set_insitu")
+
+    def insitu_read(self, batch, stream, cap=1024):
+        """Per slice, per op index: the launch times the `batch`-frame forward keyed to `stream` (a
+        torch stream; a graph's capture stream) last recorded."""
+        ns = ctypes.c_int32()
+        ms = (ctypes.c_float * (cap * 8))()
+        _lib.check(_lib.lib().tv_engine_insitu_read(self._h, batch, ctypes.c_void_p(stream.cuda_stream), ms, cap,
+                                                    ctypes.byref(ns)), "insitu_read")
+        return [[ms[k * cap + i] for i in range(cap)] for k in range(ns.value)]
 
     def profile(self, img, out=None, cap=4096):
         """Per-launch (label, ms, flops, kernel) of one forward, timed with HIP events. `img` is the

@@ -17,6 +17,8 @@ Extra keys next to the contract's (all measured in this run, on rank 0):
   parity           the timed precision's detections on the golden frame (inside a B-frame
                    batch) vs the reference's decode(K=100) records (tests/golden/detcmp.py)
   fp32_value       frames/s of the same step in fp32 (the reference's arithmetic)
+  fp32x3           the same in precision "fp32x3" (fp32 operands, each pipelined conv product as three
+                   fp16 MFMAs) and its heads' max relative difference from the fp32 engine's
   latency_b1       B=1 hipGraph replay (forward + decode + D2H), in fp16 and in bf16
   host_feed        frames/s when the u8 frames start in pinned host memory (H2D on a
                    side stream, double-buffered, overlapped with the previous step)
@@ -187,7 +189,8 @@ def insitu_launch_ms(eng, inp, out, idx, n_ops, reps):
     """Mean in-situ duration (ms) of launches `idx` over all concurrent slices of one forward of
     `inp`, timed as the timed region runs it: the forward captured as a hipGraph (its slices'
     fork / join and an event record node before every launch on its slice's stream:
-    engine.set_insitu) and replayed, `reps` replays, the median of their means. Returns (ms, how);
+    engine.set_insitu) and replayed `reps` times: the mean over all those launches (the two slices
+    overlap differently from replay to replay, as in the timed region). Returns (ms, how);
     if the runtime cannot time graph-recorded events, the eager forward with the same events
     (engine.profile_insitu) stands in."""
     dev = inp.device
@@ -210,13 +213,12 @@ def insitu_launch_ms(eng, inp, out, idx, n_ops, reps):
             eng.set_insitu(False)
         g.replay()
         torch.cuda.synchronize(dev)
-        per_rep = []
+        d = []
         for _ in range(reps):
             g.replay()
             torch.cuda.synchronize(dev)
-            d = [t[i] for t in eng.insitu_read(B, st, cap=n_ops) for i in idx]
-            per_rep.append(sum(d) / len(d))
-        return float(np.median(per_rep)), "graph"
+            d += [t[i] for t in eng.insitu_read(B, st, cap=n_ops) for i in idx]
+        return float(np.mean(d)), "graph"
     except RuntimeError as e:
         print(f"bench.py: in-situ graph timing unavailable ({e}); eager in-situ pass instead", file=sys.stderr)
     eng.profile_insitu(inp, out, cap=n_ops)
@@ -267,7 +269,7 @@ def conv_roofline(pipe, frames, precision, reps=5, model="r18"):
     # duration (median over `reps` forwards); the isolated passes above stay as *_isolated.
     idx = [i for i, o in enumerate(best) if o[2] > 0 and o[3] == name]
     ms_situ, how = insitu_launch_ms(pipe.eng, frames[:pipe.B].contiguous(), pipe.eng.alloc_out(pipe.B), idx,
-                                    len(best), reps)
+                                    len(best), 4 * reps)
     achieved = flops / n / (ms_situ * 1e-3) / 1e12
     all_ms = sum(o[1] for o in conv)
     all_fl = sum(o[2] for o in conv)
@@ -275,7 +277,7 @@ def conv_roofline(pipe, frames, precision, reps=5, model="r18"):
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "timing": (f"in situ ({how}): mean launch duration over the {pipe.B}-frame forward's concurrent "
-                       f"slices as the timed region runs it, median of {reps} replays ({ms_situ:.4f} ms); "
+                       f"slices as the timed region runs it, mean over {4 * reps} replays ({ms_situ:.4f} ms); "
                        f"*_isolated: one slice's launches serialised, median of {reps} passes (best: their "
                        f"minimum)"),
             "launch_ms": round(ms_situ, 4),
@@ -477,13 +479,29 @@ def node_leg(device, steps):
     return out
 
 
-def fp32_throughput(arch, mc, B, K, thr, device, frames, steps):
+def fp32_throughput(arch, mc, B, K, thr, device, frames, steps, precision="fp32"):
     """the same step in fp32 on a freshly built model: >= 10 timed steps after 3 warm-ups (round 3
     timed 3 after 1, and the number was bimodal across boxes)"""
-    model, oc, _ = build_model("fp32", device, arch)
+    model, oc, _ = build_model(precision, device, arch)
     pipe = Pipeline(model, oc, mc, B, K, thr, device)
     el = timed(lambda: pipe.step(frames), max(10, steps), 3)
-    return round(B * steps / el, 2)
+    return round(B * max(10, steps) / el, 2)
+
+
+def fp32x3_leg(arch, mc, B, K, thr, device, frames, steps):
+    """precision="fp32x3" (each pipelined conv product as three fp16 MFMAs on fp32 operands): the
+    step's frames/s, and its heads against the exact-fp32 engine's on the first 4 bench frames
+    (max |difference| / max |fp32 value| per head tensor)"""
+    value = fp32_throughput(arch, mc, B, K, thr, device, frames, steps, "fp32x3")
+    outs = {}
+    for prec in ("fp32", "fp32x3"):
+        model, oc, _ = build_model(prec, device, arch)
+        eng = model.engine(device, mc.in_h, mc.in_w)
+        outs[prec] = eng.forward_u8(frames[:4].contiguous()).float()
+        del model, eng
+    ref, got = outs["fp32"], outs["fp32x3"]
+    rel = float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30))
+    return {"value": value, "max_rel_diff_vs_fp32": rel, "frames_compared": 4}
 
 
 def cpu_model():
@@ -664,12 +682,12 @@ def run_yolact(args, world, rank, device):
             ks.setdefault(kname, []).append((i, ms_i, fl_i))
     sname, sl = max(ks.items(), key=lambda kv: sum(t[1] for t in kv[1]))
     idx = [t[0] for t in sl]
-    ms_situ, how = insitu_launch_ms(eng, x, proto, idx, len(prof_s), 5)
+    ms_situ, how = insitu_launch_ms(eng, x, proto, idx, len(prof_s), 20)
     ach = sum(t[2] for t in sl) / len(sl) / (ms_situ * 1e-3) / 1e12
     roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(ach / peak, 4), "launch_ms": round(ms_situ, 4),
             "timing": (f"in situ ({how}): {sname}'s mean launch duration over the forward's concurrent "
-                       f"slices, median of 5 replays; *_isolated: the whole batch's launches serialised"),
+                       f"slices, mean over 20 replays; *_isolated: the whole batch's launches serialised"),
             "achieved_isolated": round(fl / (ms * 1e-3) / 1e12, 2),
             "frac_isolated": round(fl / (ms * 1e-3) / 1e12 / peak, 4),
             "traffic": load_traffic(name, B, args.precision, "yolact"), "launch_batch": B,
@@ -943,6 +961,8 @@ def main():
         del pipe
         torch.cuda.synchronize()
         extras["fp32_value"] = fp32_throughput(args.model, mc, B, K, args.thr, device, frames, args.fp32_steps)
+        torch.cuda.synchronize()
+        extras["fp32x3"] = fp32x3_leg(args.model, mc, B, K, args.thr, device, frames, args.fp32_steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

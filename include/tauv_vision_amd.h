@@ -38,7 +38,11 @@ extern "C" {
 #define TV_ENOTFOUND 4 /* missing state_dict key */
 #define TV_ENOMEM 5
 
-typedef enum tv_dtype { TV_F32 = 0, TV_F16 = 1, TV_BF16 = 2 } tv_dtype;
+/* TV_F32X3: fp32 activations and weights, each conv product on the pipelined implicit GEMM as three
+ * fp16 MFMAs (hi = fp16(x), lo = fp16(x - hi): a_hi*b_hi + a_hi*b_lo + a_lo*b_hi, fp32 accumulation,
+ * ~22-bit operands): within the fp32 path's 1e-4 golden tolerance, ~2x its throughput; TV_F32 is the
+ * exact-f32 MFMA path. */
+typedef enum tv_dtype { TV_F32 = 0, TV_F16 = 1, TV_BF16 = 2, TV_F32X3 = 3 } tv_dtype;
 
 /* Model description: the fields of ModelConfig (config.py:6-35) plus the head list of
  * get_head_channels() (centernet.py:114-142). `arch` selects the network family:
@@ -65,7 +69,7 @@ typedef struct tv_model_desc {
   int32_t n_heads;
   int32_t head_channels[16]; /* get_head_channels(object_config) */
   int32_t in_h, in_w;        /* ModelConfig.in_h / in_w */
-  int32_t compute_dtype;     /* tv_dtype: TV_F32 = exact-f32 parity mode */
+  int32_t compute_dtype;     /* tv_dtype: TV_F32 = exact-f32 parity mode, TV_F32X3 its three-fp16-MFMA form */
   int32_t arch;              /* TV_ARCH_* */
 } tv_model_desc;
 

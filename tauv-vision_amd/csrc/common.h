@@ -108,7 +108,9 @@ struct ConvParams {
 
 // Pipelined variant (conv_pipe.hip): 256-pixel tiles, LDS-DMA ring; needs ConvParams.ks.
 int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
-                     hipStream_t s);
+                     hipStream_t s, int x3 = 0);
+// fp32 weights [Npad][Kpad] -> conv_pipe's X3 copy (x3 launches: fp32 products as three fp16 MFMAs)
+int conv_pipe_x3_repack(const void* w, int Npad, int Kpad, void* out, hipStream_t s);
 constexpr int kPipeTileM = 256;
 // Split-K variant for the small levels (conv_lat.hip): 64-pixel x 128-channel tiles, the k-step
 // descriptors split over two 4-wave K groups; ConvParams.mtiles / ntiles from conv_lat_tiles();

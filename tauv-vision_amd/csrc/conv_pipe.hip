@@ -55,8 +55,17 @@ __device__ __forceinline__ u32x4 ds_read16_off(unsigned addr) {
 
 __device__ __forceinline__ uint4 to_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
 
-template <typename T, typename OutT, int MODE>
+// X3 (T = float only): fp32 operands, products as three fp16 MFMAs — a = a_hi + a_lo, b = b_hi + b_lo
+// with hi = fp16(x), lo = fp16(x - hi) (22 significant bits), a*b = a_hi*b_hi + a_hi*b_lo + a_lo*b_hi
+// (+ a_lo*b_lo ~ 2^-22 relative, dropped) accumulated in fp32: v_mfma_f32_32x32x16_f16 at 16x the
+// MACs per instruction of v_mfma_f32_32x32x2_f32, three of them per product. The weights come
+// pre-split (conv_pipe_x3_repack: per group of 8 K values 16 B of hi halves then 16 B of lo halves,
+// the same bytes per row as fp32); the activation fragments are split in registers per sub-step.
+// Lane half lh of sub-step s reads chunks 4s + 2lh (+1): K group 2s + lh of the 32-deep k-step in
+// both operands (hi / lo halves of the weights, two 4-float chunks of the activations).
+template <typename T, typename OutT, int MODE, bool X3 = false>
 __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict__ pp, void* out_ptr) {
+  static_assert(!X3 || sizeof(T) == 4, "X3: fp32 operands");
   const ConvParams& p = *pp;
   constexpr int VEC = 16 / sizeof(T);
   constexpr int BK = ROWB / sizeof(T);
@@ -193,7 +202,7 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   const unsigned lds0 = (unsigned)(uintptr_t)lds;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = 2 * j + lh;
+    const int c = X3 ? 4 * (j >> 1) + 2 * lh + (j & 1) : 2 * j + lh;
     xaddr[j] = lds0 + xr * ROWB + ((c ^ ((xr >> 1) & 7)) << 4);
     waddr[j] = lds0 + A_BYTES + wr * ROWB + ((c ^ ((wr >> 1) & 7)) << 4);
   }
@@ -219,12 +228,37 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
     }
   };
   auto mfmas = [&](const u32x4(&f)[4][4]) __attribute__((always_inline)) {
+    if constexpr (X3) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int st = 0; st < 2; ++st) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {  // one split activation fragment live at a time
+          const u32x4 c0 = f[2 * st][2 + b], c1 = f[2 * st + 1][2 + b];
+          const float v[8] = {__uint_as_float(c0.x), __uint_as_float(c0.y), __uint_as_float(c0.z), __uint_as_float(c0.w),
+                              __uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z), __uint_as_float(c1.w)};
+          half8 xh, xl;
 #pragma unroll
-        for (int b = 0; b < 2; ++b) Mfma<T>::run(to_u4(f[j][a]), to_u4(f[j][2 + b]), acc[a][b]);
+          for (int e = 0; e < 8; ++e) {
+            xh[e] = (_Float16)v[e];
+            xl[e] = (_Float16)(v[e] - (float)xh[e]);
+          }
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            const half8 wh = __builtin_bit_cast(half8, f[2 * st][a]), wl = __builtin_bit_cast(half8, f[2 * st + 1][a]);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, acc[a][b], 0, 0, 0);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) Mfma<T>::run(to_u4(f[j][a]), to_u4(f[j][2 + b]), acc[a][b]);
+    }
   };
   KStep dn;  // descriptor of the next k-step to issue
   // one k-step: stage ks's fragments are in `cur`; DMA keeps stages ks+2, ks+3 in flight
@@ -428,10 +462,10 @@ __global__ __launch_bounds__(NT, 2) void conv_pipe(const ConvParams* __restrict_
   }
 }
 
-template <typename T, typename OutT, int MODE>
+template <typename T, typename OutT, int MODE, bool X3 = false>
 static int launch_pipe_t(const ConvParams& p, const ConvParams* dp, void* out, hipStream_t s) {
-  auto k = conv_pipe<T, OutT, MODE>;
-  if (int r = ensure_lds<conv_pipe<T, OutT, MODE>>(LDS)) return r;
+  auto k = conv_pipe<T, OutT, MODE, X3>;
+  if (int r = ensure_lds<conv_pipe<T, OutT, MODE, X3>>(LDS)) return r;
   const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
   if (ksplit > 1 && (!p.slab || !p.cnt || ksplit > p.nks)) return 1;  // TV_EINVAL
   hipLaunchKernelGGL(k, dim3(p.mtiles * p.ntiles * ksplit), dim3(NT), LDS, s, dp, out);
@@ -439,12 +473,40 @@ static int launch_pipe_t(const ConvParams& p, const ConvParams* dp, void* out, h
   return 0;
 }
 
+// [Npad][Kpad] fp32 -> the X3 weight copy: per row, per group of 8 K values, 8 hi then 8 lo halves
+__global__ void x3_repack(const float* __restrict__ w, long groups, uint4* __restrict__ out) {
+  for (long g = (long)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += (long)gridDim.x * blockDim.x) {
+    half8 h, l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = w[g * 8 + e];
+      h[e] = (_Float16)v;
+      l[e] = (_Float16)(v - (float)h[e]);
+    }
+    out[2 * g] = __builtin_bit_cast(uint4, h);
+    out[2 * g + 1] = __builtin_bit_cast(uint4, l);
+  }
+}
+
 }  // namespace pipe
 
+int conv_pipe_x3_repack(const void* w, int Npad, int Kpad, void* out, hipStream_t s) {
+  if (Kpad % 8 || !w || !out) {
+    set_error("conv_pipe_x3_repack: Kpad must be a multiple of 8");
+    return 1;
+  }
+  hipLaunchKernelGGL(pipe::x3_repack, dim3(256), dim3(256), 0, s, (const float*)w, (long)Npad * Kpad / 8, (uint4*)out);
+  TV_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_conv_pipe(const ConvParams& p, const ConvParams* dp, void* out, int dtype, int out_f32, int mode,
-                     hipStream_t s) {
+                     hipStream_t s, int x3) {
   using namespace pipe;
   if (dtype == F32) {
+    if (x3)
+      return mode == 0 ? launch_pipe_t<float, float, 0, true>(p, dp, out, s)
+                       : launch_pipe_t<float, float, 1, true>(p, dp, out, s);
     return mode == 0 ? launch_pipe_t<float, float, 0>(p, dp, out, s) : launch_pipe_t<float, float, 1>(p, dp, out, s);
   } else if (dtype == F16) {
     if (mode == 1) return launch_pipe_t<_Float16, _Float16, 1>(p, dp, out, s);

@@ -284,8 +284,12 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
                    const std::vector<std::pair<std::string, std::string>>& knobs) {
   desc = d;
   device = dev;
-  dtype = d.compute_dtype;
-  int rc = build_plan(d, &plan);
+  if (desc.compute_dtype == TV_F32X3) {  // fp32 storage; the pipelined GEMMs' products as three fp16 MFMAs
+    desc.compute_dtype = TV_F32;
+    f32x3 = 1;
+  }
+  dtype = desc.compute_dtype;
+  int rc = build_plan(desc, &plan);
   if (rc) return rc;
   for (int i = 0; i < n; ++i) {
     if (!w[i].name || (!w[i].data && w[i].numel)) {
@@ -323,6 +327,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_PIPE_SPLIT") pipe_split_mode = std::max(0, std::min(2, v));
     else if (k == "TV_PIPE_SPLIT_MAX") pipe_split_max = std::max(1, std::min(64, v));
     else if (k == "TV_PIPE_SPLIT_RED") pipe_split_red = std::max(0, v);
+    else if (k == "TV_F32X3") f32x3 = v ? 1 : 0;
     else if (k == "TV_LATGROUP") lat_group = v ? 1 : 0;
     else if (k == "TV_CT3") ct3_mode = v ? 1 : 0;
     else if (k == "TV_BURST") burst_mode = std::max(0, std::min(2, v));
@@ -434,6 +439,7 @@ Engine::~Engine() {
     if (p.w_c3e) (void)hipFree(p.w_c3e);
     if (p.w_ss2) (void)hipFree(p.w_ss2);
     if (p.w_burst) (void)hipFree(p.w_burst);
+    if (p.w_x3) (void)hipFree(p.w_x3);
     if (p.w_ct3) (void)hipFree(p.w_ct3);
     if (p.head_w) (void)hipFree(p.head_w);
     if (p.head_b) (void)hipFree(p.head_b);
@@ -1173,6 +1179,20 @@ int Engine::make_workspace(int B, Workspace* ws) {
         }
     }
   }
+  // fp32 X3: the pipelined layers read the hi / lo fp16 copy of their weights
+  if (dtype == F32 && f32x3) {
+    for (size_t i = 0; i < nops; ++i) {
+      if (!ws->use_pipe[i]) continue;
+      Packed& pk = packed[i];
+      if (!pk.w_x3) {
+        TV_HIP(hipMalloc(&pk.w_x3, (size_t)pk.Npad * pk.Kpad * 4));
+        int rc = conv_pipe_x3_repack(pk.w, pk.Npad, pk.Kpad, pk.w_x3, nullptr);
+        if (rc) return rc;
+        TV_HIP(hipDeviceSynchronize());
+      }
+      ws->params[i].weight = pk.w_x3;
+    }
+  }
   if (!all_ks.empty()) {
     TV_HIP(hipMalloc((void**)&ws->dks, all_ks.size() * sizeof(KStep)));
     TV_HIP(hipMemcpy(ws->dks, all_ks.data(), all_ks.size() * sizeof(KStep), hipMemcpyHostToDevice));
@@ -1335,7 +1355,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
                                            ws->c3_res[i], ws->c3_ni[i], ws->c3_nw[i])
-           : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s)
+           : ws->use_pipe[i] ? launch_conv_pipe(p, ws->dparams + i, p.out, dtype, out_f32, mode, s, dtype == F32 && f32x3)
                              : launch_conv(p, ws->dparams + i, p.out, dtype, out_f32, mode, s);
   if (rc) return rc;
   if (op.kind == OP_CONVT_ADD) {
@@ -1605,7 +1625,8 @@ const char* Engine::op_kernel(int B, size_t i) {
       else if (ws->s2_grid[i]) name = std::string("tv::c3s2::conv3x3s2<") + t + ", " + std::to_string(op.act) + ">";
       else if (ws->c3_tw[i]) name = std::string("tv::c3::conv3x3<") + t + ", " + t + ", " + std::to_string(ws->c3_tw[i]) + ", " + std::to_string(op.act) + ", " + std::to_string(ws->head_fused[i]) + ", " + std::to_string(ws->c3_res[i]) + ", " + std::to_string(ws->c3_ni[i]) + ", " + std::to_string(plan.tensors[op.segs[0].src].C / 32) + ", " + std::to_string(ws->c3_nw[i]) + ">";
       else if (ws->use_pipe[i]) {
-        name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) + ">";
+        name = std::string("tv::pipe::conv_pipe<") + t + ", " + o + ", " + std::to_string(mode) +
+               (dtype == F32 && f32x3 ? ", true>" : ">");
         if (ws->params[i].ksplit > 1) name += " split-K " + std::to_string(ws->params[i].ksplit);
       }
       else name = std::string("tv::conv_igemm<") + t + ", " + o + ", " + std::to_string(mode) + ">";

@@ -18,6 +18,7 @@ struct Packed {
   void* w_c3e = nullptr;   // conv3x3.hip copy for the fused-heads body when its swizzle differs (conv3x3_k16)
   void* w_ss2 = nullptr;   // stem_s2.hip k-step-ordered copy of block0.conv1's weights (made on first use)
   void* w_burst = nullptr; // conv_burst.hip [32-channel tile][k-step][lane] copy (made on first use)
+  void* w_x3 = nullptr;    // conv_pipe.hip X3 copy of the fp32 weights: hi / lo fp16 halves (made on first use)
   void* w_ct3 = nullptr;   // convt3.hip fragments of a whole ConvTranspose2d(3, s2) (its phase-(0,0) op)
   float* bias = nullptr;   // [Npad]
   int Npad = 0, Kpad = 0;
@@ -111,6 +112,8 @@ struct Engine {
   int burst_mode = 1;          // conv_burst.hip for the small conv_lat layers it represents (knob TV_BURST=0 off,
                                // 2 = every layer it represents: diagnostics / tests)
   int lat_split_max = 4;       // conv_lat workgroups per tile (split-K) on under-filled layers (knob TV_LAT_SPLIT, 1 = off)
+  int f32x3 = 0;               // fp32 engines: conv_pipe products as three fp16 MFMAs (hi/lo split, ~22-bit
+                               // operands, fp32 accumulation) instead of v_mfma_f32_32x32x2_f32 (knob TV_F32X3)
   int pipe_split_mode = 1;     // conv_pipe split-K on under-filled layers: 0 off, 1 fp32 only, 2 every dtype (TV_PIPE_SPLIT)
   int pipe_split_max = 16;     // ... at most this many slices per tile (knob TV_PIPE_SPLIT_MAX)
   int pipe_split_red = 5;      // ... hand-off cost per slice in tenths of a k-step (knob TV_PIPE_SPLIT_RED)

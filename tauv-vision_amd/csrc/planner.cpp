@@ -321,7 +321,10 @@ struct Walker {
 
 }  // namespace
 
-int build_plan(const tv_model_desc& d, Plan* plan) {
+int build_plan(const tv_model_desc& d0, Plan* plan) {
+  // TV_F32X3 plans as TV_F32 (fp32 storage; only the engine's GEMM kernel choice differs)
+  tv_model_desc d = d0;
+  if (d.compute_dtype == TV_F32X3) d.compute_dtype = TV_F32;
   if (d.arch == TV_ARCH_DLA34) return build_plan_dla34(d, plan);
   if (d.arch == TV_ARCH_PROTONET) return build_plan_protonet(d, plan);
   if (d.arch != TV_ARCH_CENTERNET && d.arch != TV_ARCH_CENTERNET_BACKBONE) {

@@ -11,7 +11,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtauv_vision_amd.so")
 
 TV_OK, TV_EINVAL, TV_ESHAPE, TV_EHIP, TV_ENOTFOUND, TV_ENOMEM = range(6)
-DTYPES = {"fp32": 0, "fp16": 1, "bf16": 2}
+DTYPES = {"fp32": 0, "fp16": 1, "bf16": 2, "fp32x3": 3}  # fp32x3: fp32 with each product as three fp16 MFMAs
 
 c_i32, c_i64, c_f32, c_f64, c_vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_double, ctypes.c_void_p
 

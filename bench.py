@@ -233,12 +233,12 @@ def conv_roofline(pipe, frames, precision, reps=5, model="r18"):
     """Per-launch HIP-event timing. The timed path launches a B-frame forward as concurrent
     slices (engine.slices). The dominant kernel is the conv instance with the largest summed time
     in one slice's serialised pass (tv_engine_profile: events around every launch on the launch
-    stream, `reps` passes: the per-op times of BENCH_PROFILE_OUT and `*_isolated` / `*_best`).
-    `achieved` = its algorithmic FLOPs per launch (2*MAC) / its average launch
-    duration IN SITU: the B-frame forward captured with an event before every launch on its
-    slice's stream and replayed as the timed region replays its graph (insitu_launch_ms), so the
-    duration includes the CUs the other slice holds meanwhile — what rocprofv3's kernel trace of
-    the timed region reports."""
+    stream, `reps` passes: the per-op times of BENCH_PROFILE_OUT). `achieved` = its algorithmic
+    FLOPs per launch (2*MAC) / its median serialised launch duration (the kernel with
+    the chip to itself); `*_insitu` = the same over its launches in the B-frame forward replayed as
+    the timed region runs it, with an event record node before every launch (insitu_launch_ms):
+    durations stretched by the CUs the concurrent slice holds, and by the event nodes themselves
+    (rocprofv3's timed-region durations sit between the two: DESIGN.md §5)."""
     bs = pipe.eng.slices(pipe.B)[0]
     fr = frames[:bs].contiguous()
     out = pipe.eng.alloc_out(bs)
@@ -270,25 +270,26 @@ def conv_roofline(pipe, frames, precision, reps=5, model="r18"):
     idx = [i for i, o in enumerate(best) if o[2] > 0 and o[3] == name]
     ms_situ, how = insitu_launch_ms(pipe.eng, frames[:pipe.B].contiguous(), pipe.eng.alloc_out(pipe.B), idx,
                                     len(best), 4 * reps)
-    achieved = flops / n / (ms_situ * 1e-3) / 1e12
+    achieved_situ = flops / n / (ms_situ * 1e-3) / 1e12
+    achieved = achieved_iso
     all_ms = sum(o[1] for o in conv)
     all_fl = sum(o[2] for o in conv)
     top = sorted(best, key=lambda o: -o[1])[:6]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
-            "timing": (f"in situ ({how}): mean launch duration over the {pipe.B}-frame forward's concurrent "
-                       f"slices as the timed region runs it, mean over {4 * reps} replays ({ms_situ:.4f} ms); "
-                       f"*_isolated: one slice's launches serialised, median of {reps} passes (best: their "
-                       f"minimum)"),
-            "launch_ms": round(ms_situ, 4),
-            "achieved_isolated": round(achieved_iso, 2), "frac_isolated": round(achieved_iso / peak, 4),
+            "timing": (f"one slice's launches serialised, median of {reps} passes (best: their minimum); "
+                       f"*_insitu ({how}): the {pipe.B}-frame forward captured with an event record node before "
+                       f"every launch and replayed as the timed region runs (concurrent slices), mean over "
+                       f"{4 * reps} replays ({ms_situ:.4f} ms per launch)"),
+            "launch_ms": round(ms / n, 4), "launch_ms_insitu": round(ms_situ, 4),
+            "achieved_insitu": round(achieved_situ, 2), "frac_insitu": round(achieved_situ / peak, 4),
             "achieved_best": round(achieved_best, 2), "frac_best": round(achieved_best / peak, 4),
             # the PMC profile is of one pipe.B-frame forward (its launches are the same per-slice
             # launches timed here), so it is looked up by the forward batch
             "traffic": load_traffic(name, pipe.B, precision, model),
             "launch_batch": bs,
-            "kernel": (f"{name}: {n} launches per slice forward, avg {ms_situ:.4f} ms in situ ({ms / n:.4f} ms "
-                       f"isolated), avg {flops / n / 1e9:.2f} GFLOP/launch"),
+            "kernel": (f"{name}: {n} launches per slice forward, avg {ms / n:.4f} ms serialised ({ms_situ:.4f} ms "
+                       f"in situ), avg {flops / n / 1e9:.2f} GFLOP/launch"),
             "all_conv": {"launches": len(conv), "ms": round(all_ms, 3), "tflops": round(all_fl / all_ms / 1e9, 1)},
             "per_kernel": {k: {"launches": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / v[1] / 1e9, 1)}
                            for k, v in kern.items()},
@@ -455,15 +456,15 @@ def node_leg(device, steps):
     normalised [1, 3, 480, 640] fp32 image on the device -> `model(img)` -> `decode_keypoints(
     prediction, model_config, object_config, M_projection, n_detections=10, keypoint_n_detections=50,
     score_threshold=0.6, keypoint_score_threshold=0.3, keypoint_angle_threshold=0.3)` (a host list of
-    detections) per frame; the drop-in default precision fp32 and fp16, with the forward's graph
-    cache (default) and eager."""
+    detections) per frame; the drop-in default precision fp32, fp32x3 and fp16, with the forward's
+    graph cache (default) and eager."""
     from tauv_vision_amd.decode import decode_keypoints
     mc = tv.ModelConfig(HEIGHTS, CHANNELS, 480, 640, DOWNSAMPLES, 1.0)
     M = np.array([[307.0, 0.0, 160.0], [0.0, 307.0, 120.0], [0.0, 0.0, 0.0]])
     img = torch.randn((1, 3, 480, 640), generator=torch.Generator().manual_seed(5)).to(device)
     out = {"model": "CenterpointDLA34 (centernet_node.py:46), keypoint heads", "batch": 1,
            "call": "model(img) -> decode_keypoints(K=10/50, thr 0.6/0.3), host detections"}
-    for prec in ("fp32", "fp16"):
+    for prec in ("fp32", "fp32x3", "fp16"):
         model, oc, _ = build_model(prec, device, "dla34")
         r = {}
         for mode, replay in (("replay_ms", True), ("eager_ms", False)):
@@ -684,12 +685,12 @@ def run_yolact(args, world, rank, device):
     idx = [t[0] for t in sl]
     ms_situ, how = insitu_launch_ms(eng, x, proto, idx, len(prof_s), 20)
     ach = sum(t[2] for t in sl) / len(sl) / (ms_situ * 1e-3) / 1e12
-    roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4), "launch_ms": round(ms_situ, 4),
-            "timing": (f"in situ ({how}): {sname}'s mean launch duration over the forward's concurrent "
-                       f"slices, mean over 20 replays; *_isolated: the whole batch's launches serialised"),
-            "achieved_isolated": round(fl / (ms * 1e-3) / 1e12, 2),
-            "frac_isolated": round(fl / (ms * 1e-3) / 1e12 / peak, 4),
+    roof = {"bound": "mfma", "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4),
+            "timing": (f"the whole batch's launches serialised; *_insitu ({how}): {sname}'s mean launch duration "
+                       f"over the forward's concurrent slices (event record nodes, graph replays), 20 replays"),
+            "launch_ms_insitu": round(ms_situ, 4),
+            "achieved_insitu": round(ach, 2), "frac_insitu": round(ach / peak, 4),
             "traffic": load_traffic(name, B, args.precision, "yolact"), "launch_batch": B,
             "kernel": f"{name}: {n} launches/forward, avg {ms / n:.4f} ms, avg {fl / n / 1e9:.2f} GFLOP/launch",
             "per_kernel": {kn: {"launches": v[0], "ms": round(v[1], 3), "tflops": round(v[2] / v[1] / 1e9, 1)}

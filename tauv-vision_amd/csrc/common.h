@@ -116,7 +116,7 @@ constexpr int kPipeTileM = 256;
 // descriptors split over two 4-wave K groups; ConvParams.mtiles / ntiles from conv_lat_tiles();
 // mode-0 k-steps only (every segment's channel count a multiple of 64 / 128 bytes)
 int conv_lat_tiles(int M, int N, int* mtiles, int* ntiles);
-int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s);
+int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s, int x3 = 0);
 // One-shot small-level conv (conv_burst.hip): 64 output pixels (raster, one frame) x 32 channels
 // per 256-thread workgroup, K split over its 4 waves (<= 20 k-steps of 16 each, weights in
 // registers), every input the tile reads staged in LDS at once. Segments: 3x3 / stride 1 / pad 1
@@ -164,7 +164,8 @@ bool conv1x1_stream_supported(const ConvParams& p, int esz);
 int launch_conv1x1_stream(const ConvParams& p, const ConvParams* dp, int dtype, int cu_count, hipStream_t s);
 constexpr int kLatGroupMax = 4;  // layers per grouped conv_lat launch
 // independent layers in one launch (hp: host copies for validation, dp: their device copies)
-int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* dp, int n, int dtype, hipStream_t s);
+int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* dp, int n, int dtype, hipStream_t s,
+                          int x3 = 0);
 // fp32 slab floats one conv_lat split-K tile slice needs (64 x 128)
 constexpr int kLatSlabFloats = 64 * 128;
 

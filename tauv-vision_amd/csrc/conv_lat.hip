@@ -53,7 +53,7 @@ __device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int au
 __device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 
 // one workgroup's tile (or split-K slice of a tile) of the layer *pp; bid = its index in the layer
-template <typename T>
+template <typename T, bool X3 = false>  // X3: fp32 operands, products as three fp16 MFMAs (conv_pipe.hip X3)
 __device__ __forceinline__ void conv_lat_tile(const ConvParams* __restrict__ pp, const int bid) {
   const ConvParams& p = *pp;
   constexpr int VEC = 16 / sizeof(T);
@@ -170,7 +170,7 @@ __device__ __forceinline__ void conv_lat_tile(const ConvParams* __restrict__ pp,
   const unsigned lds0 = (unsigned)(uintptr_t)ring;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = 2 * j + lh;
+    const int c = X3 ? 4 * (j >> 1) + 2 * lh + (j & 1) : 2 * j + lh;  // X3: lane half lh of sub-step pair s = K group 2s + lh
     xaddr[j] = lds0 + xr * ROWB + ((c ^ ((xr >> 1) & 7)) << 4);
     waddr[j] = lds0 + A_BYTES + wr * ROWB + ((c ^ ((wr >> 1) & 7)) << 4);
   }
@@ -186,10 +186,32 @@ __device__ __forceinline__ void conv_lat_tile(const ConvParams* __restrict__ pp,
     }
   };
   auto mfmas = [&](const u32x4(&f)[4][3]) __attribute__((always_inline)) {
+    if constexpr (X3) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int st = 0; st < 2; ++st) {
+        const u32x4 c0 = f[2 * st][2], c1 = f[2 * st + 1][2];
+        const float v[8] = {__uint_as_float(c0.x), __uint_as_float(c0.y), __uint_as_float(c0.z), __uint_as_float(c0.w),
+                            __uint_as_float(c1.x), __uint_as_float(c1.y), __uint_as_float(c1.z), __uint_as_float(c1.w)};
+        half8 xh, xl;
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) Mfma<T>::run(to_u4(f[j][nb]), to_u4(f[j][2]), acc[nb]);
+        for (int e = 0; e < 8; ++e) {
+          xh[e] = (_Float16)v[e];
+          xl[e] = (_Float16)(v[e] - (float)xh[e]);
+        }
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          const half8 wh = __builtin_bit_cast(half8, f[2 * st][nb]), wl = __builtin_bit_cast(half8, f[2 * st + 1][nb]);
+          acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc[nb], 0, 0, 0);
+          acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, acc[nb], 0, 0, 0);
+          acc[nb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, acc[nb], 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) Mfma<T>::run(to_u4(f[j][nb]), to_u4(f[j][2]), acc[nb]);
+    }
   };
   // iteration j (both groups run `half` iterations so every wave meets every barrier; group 1
   // idles through its last one when nks is odd): stage j's fragments are in `cur`
@@ -364,9 +386,9 @@ __device__ __forceinline__ void conv_lat_tile(const ConvParams* __restrict__ pp,
   }
 }
 
-template <typename T>
+template <typename T, bool X3 = false>
 __global__ __launch_bounds__(NT, 1) void conv_lat(const ConvParams* __restrict__ pp) {
-  conv_lat_tile<T>(pp, blockIdx.x);
+  conv_lat_tile<T, X3>(pp, blockIdx.x);
 }
 
 // several independent layers in one launch (the engine's schedule: layers of one dependency
@@ -376,26 +398,26 @@ struct LatGroup {
   int end[kLatGroupMax];
   int n;
 };
-template <typename T>
+template <typename T, bool X3 = false>
 __global__ __launch_bounds__(NT, 1) void conv_lat_group(const LatGroup g) {
   const int b = blockIdx.x;
   int k = 0;
   while (k + 1 < g.n && b >= g.end[k]) ++k;  // (workgroup-uniform)
-  conv_lat_tile<T>(g.p[k], b - (k ? g.end[k - 1] : 0));
+  conv_lat_tile<T, X3>(g.p[k], b - (k ? g.end[k - 1] : 0));
 }
 
-template <typename T>
+template <typename T, bool X3 = false>
 static int launch_group_t(const LatGroup& g, hipStream_t s) {
-  if (int r = ensure_lds<conv_lat_group<T>>(LDS)) return r;
-  hipLaunchKernelGGL(conv_lat_group<T>, dim3(g.end[g.n - 1]), dim3(NT), LDS, s, g);
+  if (int r = ensure_lds<conv_lat_group<T, X3>>(LDS)) return r;
+  hipLaunchKernelGGL((conv_lat_group<T, X3>), dim3(g.end[g.n - 1]), dim3(NT), LDS, s, g);
   TV_HIP(hipGetLastError());
   return 0;
 }
 
-template <typename T>
+template <typename T, bool X3 = false>
 static int launch_t(const ConvParams& p, const ConvParams* dp, hipStream_t s) {
-  if (int r = ensure_lds<conv_lat<T>>(LDS)) return r;
-  hipLaunchKernelGGL(conv_lat<T>, dim3(p.mtiles * p.ntiles * (p.ksplit > 1 ? p.ksplit : 1)), dim3(NT), LDS, s, dp);
+  if (int r = ensure_lds<conv_lat<T, X3>>(LDS)) return r;
+  hipLaunchKernelGGL((conv_lat<T, X3>), dim3(p.mtiles * p.ntiles * (p.ksplit > 1 ? p.ksplit : 1)), dim3(NT), LDS, s, dp);
   TV_HIP(hipGetLastError());
   return 0;
 }
@@ -413,18 +435,19 @@ static bool lat_geometry_ok(const ConvParams& p) {
          p.out_ldc % 8 == 0 && p.out_coff % 8 == 0 && p.out && !(p.ksplit > 1 && (!p.slab || !p.cnt || p.ksplit > p.nks));
 }
 
-int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s) {
+int launch_conv_lat(const ConvParams& p, const ConvParams* dp, int dtype, hipStream_t s, int x3) {
   if (!lat_geometry_ok(p)) {
     set_error("conv_lat: inconsistent launch geometry");
     return 1;
   }
   if (dtype == F16) return lat::launch_t<_Float16>(p, dp, s);
   if (dtype == BF16) return lat::launch_t<__bf16>(p, dp, s);
-  return lat::launch_t<float>(p, dp, s);
+  return x3 ? lat::launch_t<float, true>(p, dp, s) : lat::launch_t<float>(p, dp, s);
   return 1;
 }
 
-int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* dp, int n, int dtype, hipStream_t s) {
+int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* dp, int n, int dtype, hipStream_t s,
+                          int x3) {
   if (n < 1 || n > kLatGroupMax) {
     set_error("conv_lat group: 1..kLatGroupMax layers");
     return 1;
@@ -444,7 +467,7 @@ int launch_conv_lat_group(const ConvParams* const* hp, const ConvParams* const* 
   }
   if (dtype == F16) return lat::launch_group_t<_Float16>(g, s);
   if (dtype == BF16) return lat::launch_group_t<__bf16>(g, s);
-  return lat::launch_group_t<float>(g, s);
+  return x3 ? lat::launch_group_t<float, true>(g, s) : lat::launch_group_t<float>(g, s);
 }
 
 }  // namespace tv

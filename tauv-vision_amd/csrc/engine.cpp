@@ -1179,10 +1179,10 @@ int Engine::make_workspace(int B, Workspace* ws) {
         }
     }
   }
-  // fp32 X3: the pipelined layers read the hi / lo fp16 copy of their weights
+  // fp32 X3: the pipelined and conv_lat layers read the hi / lo fp16 copy of their weights
   if (dtype == F32 && f32x3) {
     for (size_t i = 0; i < nops; ++i) {
-      if (!ws->use_pipe[i]) continue;
+      if (!ws->use_pipe[i] && !ws->lat[i]) continue;
       Packed& pk = packed[i];
       if (!pk.w_x3) {
         TV_HIP(hipMalloc(&pk.w_x3, (size_t)pk.Npad * pk.Kpad * 4));
@@ -1350,7 +1350,7 @@ int Engine::run_op(size_t i, Workspace* ws, const void* input, int input_u8, flo
     const BurstParams* bp = &ws->bparams[i];
     return launch_conv_burst(&bp, 1, dtype, s);
   }
-  if (ws->lat[i]) return launch_conv_lat(p, ws->dparams + i, dtype, s);
+  if (ws->lat[i]) return launch_conv_lat(p, ws->dparams + i, dtype, s, dtype == F32 && f32x3);
   if (ws->c1x1[i]) return launch_conv1x1_stream(p, ws->dparams + i, dtype, cu_count, s);
   int rc = ws->s2_grid[i] ? launch_conv3x3s2(p, ws->dparams + i, p.out, dtype, ws->s2_grid[i], s)
            : ws->c3_tw[i] ? launch_conv3x3(p, ws->dparams + i, p.out, dtype, ws->c3_tw[i], ws->c3_grid[i], s, 0,
@@ -1433,7 +1433,7 @@ int Engine::run_all(const void* input, int input_u8, int B, float* out, hipStrea
           hp[k] = &ws->params[g[k]];
           dp[k] = ws->dparams + g[k];
         }
-        rc = launch_conv_lat_group(hp, dp, (int)g.size(), dtype, s);
+        rc = launch_conv_lat_group(hp, dp, (int)g.size(), dtype, s, dtype == F32 && f32x3);
       }
       if (rc) return rc;
     }
@@ -1612,7 +1612,7 @@ const char* Engine::op_kernel(int B, size_t i) {
         name = std::string(csm_variant(op.segs[0].stride) ? "tv::csm::conv_small_halo<" : "tv::csm::conv_small<") + t + ", " + std::to_string(plan.tensors[op.segs[0].src].C) + ", " +
                std::to_string(op.N) + ", " + std::to_string(op.segs[0].stride) + ", " + std::to_string(op.act) + ">";
       else if (ws->lat[i])
-        name = std::string("tv::lat::conv_lat<") + t + ">";
+        name = std::string("tv::lat::conv_lat<") + t + (dtype == F32 && f32x3 ? ", true>" : ">");
       else if (ws->burst[i]) {
         const int q = (ws->bparams[i].nk16 + 3) / 4;
         int kpw = 20;

@@ -54,9 +54,10 @@ def _cmp(pred, g, tol, key=None):
         assert err <= tol * scale, f"{f}: max|err| {err:.3e} > {tol} * {scale:.3g}"
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
 @pytest.mark.parametrize("name", list(dla34_index()))
-def test_dla34_fp32_matches_reference(name):
-    model, oc, mc, case = build(name, "fp32")
+def test_dla34_fp32_matches_reference(name, precision):
+    model, oc, mc, case = build(name, precision)
     with torch.no_grad():
         pred = model(dla34_input(name).cuda())
     g = golden(f"dla34_{name}")

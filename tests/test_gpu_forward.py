@@ -61,18 +61,21 @@ def _cmp(pred, g, tol, key=None):
 SMALL = [n for n in models_index() if n != "r18_c128_b1_480x640"]
 
 
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
 @pytest.mark.parametrize("name", SMALL)
-def test_forward_fp32_matches_reference(name):
-    model, oc, mc, case = build(name, "fp32")
+def test_forward_fp32_matches_reference(name, precision):
+    """fp32 and fp32x3 (the fp32 operands' products as three fp16 MFMAs) at the fp32 tolerance"""
+    model, oc, mc, case = build(name, precision)
     with torch.no_grad():
         pred = model(case_input(name).cuda())
     _cmp(pred, golden(f"model_{name}"), TOL["fp32"])
 
 
-def test_forward_fp32_full_size_r18():
+@pytest.mark.parametrize("precision", ["fp32", "fp32x3"])
+def test_forward_fp32_full_size_r18(precision):
     """The BASELINE "R18" (Centernet+DLABackbone [2]*5/[128]*6, ds 2) at 480x640."""
     name = "r18_c128_b1_480x640"
-    model, oc, mc, case = build(name, "fp32")
+    model, oc, mc, case = build(name, precision)
     pred = model(case_input(name).cuda())
     g = golden(f"model_{name}")
     _cmp(pred, g, TOL["fp32"])

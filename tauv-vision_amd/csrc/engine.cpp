@@ -875,9 +875,10 @@ int Engine::make_workspace(int B, Workspace* ws) {
       p.head_row0[t] = pk2.head_row0[t];
       p.head_nrows[t] = pk2.head_nrows[t];
     }
-    // plain stores when the tiles' head rows tile the output columns exactly once (R18: one
-    // 128-channel hidden tile per head); otherwise (DLA-34: a head's 256 hidden channels span two
-    // tiles that meet in the output) atomics onto a zeroed output
+    // plain stores when the tiles' head rows tile the output columns exactly once (one 128-channel
+    // hidden tile per head: a 64-channel backbone's 2C heads); otherwise (a head's 2C = 256 hidden
+    // channels, centernet.py:45-50 on the 128-channel "R18" and DLA-34, span two tiles that meet in
+    // the output) atomics onto a zeroed output
     {
       std::vector<int> cover(plan.out_cpad, 0);
       bool ok = true;

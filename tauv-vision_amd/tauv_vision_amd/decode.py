@@ -61,12 +61,22 @@ def _gpu(t, name):
     return _lib.require_gpu_tensor(t, name)
 
 
+def _empty_batch_check(B):
+    """The reference's heatmap_detect (decode.py:255-279, and so decode / decode_keypoints) flattens
+    the heatmap with reshape(B, -1), which torch refuses for an empty batch: the same error here."""
+    if B == 0:
+        raise RuntimeError("cannot reshape tensor of 0 elements into shape [0, -1] because the unspecified "
+                           "dimension size -1 can be any value and is ambiguous")
+
+
 def heatmap_nms(heatmap: torch.Tensor, kernel_size: int) -> torch.Tensor:
     """decode.py:239-252: keep values equal to their k x k neighbourhood max, else 0."""
     assert kernel_size >= 1 and kernel_size % 2 == 1
     heatmap = _gpu(heatmap, "heatmap")
     B, C, H, W = heatmap.shape
     out = torch.empty((B, C, H, W), dtype=torch.float32, device=heatmap.device)
+    if B == 0:  # the reference's max_pool2d returns the empty batch as is
+        return out
     _lib.check(_lib.lib().tv_heatmap_nms(ctypes.c_void_p(heatmap.data_ptr()), _lib.strides(heatmap, 4), B, C, H, W,
                                          kernel_size, 0, ctypes.c_void_p(out.data_ptr()),
                                          _lib.stream_of(heatmap.device)), "heatmap_nms")
@@ -78,6 +88,7 @@ def heatmap_detect(heatmap: torch.Tensor, n_detections: int):
     heatmap = _gpu(heatmap, "heatmap")
     B, C, H, W = heatmap.shape
     n = C * H * W
+    _empty_batch_check(B)
     if not 1 <= n_detections <= n:
         raise RuntimeError(f"selected index k out of range (k={n_detections}, n={n})")
     flat = heatmap.reshape(B, n).contiguous()
@@ -168,6 +179,7 @@ def _records_many(calls):
         for heat, size, offset, depth, K, mode, ratio, in_h, in_w, thr, aux in calls:
             heat = _gpu(heat, "heatmap")
             B, C, H, W = heat.shape
+            _empty_batch_check(B)
             dec, host = _decoder(heat.device, B, C, H, W, K)
             dec(heat, size, offset, depth, mode, ratio, in_h, in_w, thr, aux)
             host.copy_(dec.packed, non_blocking=True)

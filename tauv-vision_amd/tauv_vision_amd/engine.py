@@ -88,6 +88,8 @@ class NativeEngine:
         B = img.shape[0]
         if out is None:
             out = self.alloc_out(B)
+        if B == 0:  # an empty batch: nothing to launch (the reference's convolutions return empty outputs)
+            return out
         _lib.check(_lib.lib().tv_engine_forward(self._h, ctypes.c_void_p(img.data_ptr()), B,
                                                 ctypes.c_void_p(out.data_ptr()), _lib.stream_of(self.device)),
                    "forward")
@@ -98,6 +100,8 @@ class NativeEngine:
         B = frames.shape[0]
         if out is None:
             out = self.alloc_out(B)
+        if B == 0:
+            return out
         _lib.check(_lib.lib().tv_engine_forward_u8(self._h, ctypes.c_void_p(frames.data_ptr()), B,
                                                    ctypes.c_void_p(out.data_ptr()), _lib.stream_of(self.device)),
                    "forward_u8")

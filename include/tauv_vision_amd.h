@@ -268,7 +268,9 @@ int tv_train_keypoint_targets(const uint8_t* keypoint_valid, const int64_t* keyp
  * out: compute-dtype NHWC [B,H,W,N]. variant: 0 = fused dcn_gemm (32-channel k-steps),
  * 1 = fused dcn_gemm64 (tile by size), 2 = dcn_gemm64 with 64-pixel tiles, 3 = unfused sampling +
  * implicit GEMM (the fp32 path; the only variant for TV_F32), 4 = dcn_win (the LDS-window kernel the
- * engine uses for C == N == 64; TV_EINVAL otherwise). Synchronous; allocates. */
+ * engine uses for C == N == 64; TV_EINVAL otherwise), 5 = dcn_gemm64d (gathers two k-steps ahead),
+ * 6 / 7 / 8 = dcn_gemm64 on 64-pixel tiles with split-K over 3 / 4 / 9 tap ranges (the engine's
+ * small-batch form). Synchronous; allocates. */
 int tv_diag_dcn_conv(const void* x, const void* om, int32_t B, int32_t H, int32_t W, int32_t C, int32_t om_ldc,
                      const float* weight, const float* bias, int32_t N, int32_t act, int32_t dtype, int32_t variant,
                      void* out, void* stream);

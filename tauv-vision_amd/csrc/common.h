@@ -215,7 +215,17 @@ struct DcnParams {
   int act;
   void* out;          // [B, H, W, out_ldc], N channels
   int out_ldc, N;
+  // split-K (dcn_gemm64 only; ksplit <= 1: off): ksplit workgroups per (pixel tile, channel tile),
+  // each over a tap range; fp32 partials meet in slab (dcn_split_floats each), tickets in cnt
+  // (one per tile, zero-filled once: the last slice resets its own)
+  int ksplit;
+  float* slab;
+  unsigned* cnt;
 };
+// dcn_gemm64's tile for a layer as launch_dcn_gemm picks it (BN output channels x PX pixels) and
+// the slab floats one split layer needs
+void dcn64_tile(const DcnParams& p, int dcn64_mode, int* bn, int* px);
+long dcn_split_floats(const DcnParams& p, int dcn64_mode, int ksplit);
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad);
 // dcn64_mode: 0 dcn_gemm; 1 64-channel k-steps when C % 64 == 0 (dcn_gemm64); 2 the same on 64-pixel
 // tiles; 3 the LDS-window kernel (dcn_win) where dcn_win_supported, else as 1; 5 dcn_gemm64d (gathers two

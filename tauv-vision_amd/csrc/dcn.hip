@@ -32,7 +32,9 @@ template <int BN> constexpr int lds_bytes() { return 2 * (ABUF + wbuf<BN>()); }
 constexpr int kOOB = 0x7ff00000;          // buffer offset past any num_records (host checks the sizes)
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) unsigned gu32;  // global (never flat) agent-scope ticket words
 __device__ u32x4 raw_buffer_load_v4(i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.load.v4i32");
+__device__ void raw_buffer_store_v4(u32x4 data, i32x4 rsrc, int voffset, int soffset, int aux) __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 __device__ void raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size, int voffset,
                                     int soffset, int offset, int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
 __device__ __forceinline__ uint4 to_u4(u32x4 v) { return make_uint4(v.x, v.y, v.z, v.w); }
@@ -303,9 +305,15 @@ __global__ __launch_bounds__(NT, (min_blocks2<BN, PX>())) void dcn_gemm64(const 
   const int M = p.B * HW;
   const int G = gridDim.x, ny = p.N / BN;
   const int q = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const int m0 = (q / ny) * PX, n0 = (q % ny) * BN;
+  // split-K (ksplit > 1): the ksplit workgroups of a tile are adjacent in the XCD-contiguous order;
+  // slice sl runs taps [9 sl / ksplit, 9 (sl + 1) / ksplit) (whole taps: the sampling-state ring
+  // starts at a tap)
+  const int ksplit = p.ksplit > 1 ? p.ksplit : 1;
+  const int unit = q / ksplit, slice = q - unit * ksplit;
+  const int m0 = (unit / ny) * PX, n0 = (unit % ny) * BN;
   const int ncb = p.C / 64;
-  const int S = 9 * ncb;
+  const int k_lo = 9 * slice / ksplit, k_hi = 9 * (slice + 1) / ksplit;
+  const int S0 = k_lo * ncb, S = k_hi * ncb;
 
   i32x4 xr, wrs;
   {
@@ -451,14 +459,14 @@ __global__ __launch_bounds__(NT, (min_blocks2<BN, PX>())) void dcn_gemm64(const 
   // written at the first step of tap k - 2 (slot k % 3, last read when tap k - 3's state was
   // consumed, a barrier or more earlier) and read when step 0 of tap k is issued (the last step
   // of tap k - 1: at least one barrier after it was written).
-  load_om(0);
-  tap_state(0);
-  tap_state(1);
-  load_w(0);
+  load_om(k_lo);
+  tap_state(k_lo);
+  if (k_lo + 1 < 9) tap_state(k_lo + 1);
+  load_w(S0);
   __syncthreads();
-  read_state(0);
+  read_state(k_lo);
   load_corners(0);
-  for (int s = 0; s < S; ++s) {
+  for (int s = S0; s < S; ++s) {
     const int k = s / ncb, cb = s - k * ncb;
     produce(s);  // blends step s's corners into LDS buffer s & 1
     if (cb == 0 && k + 2 < 9) tap_state(k + 2);
@@ -471,6 +479,55 @@ __global__ __launch_bounds__(NT, (min_blocks2<BN, PX>())) void dcn_gemm64(const 
     }
     __syncthreads();  // buffer s & 1 complete; every wave's reads of buffer (s - 1) & 1 are done
     consume(s);
+  }
+
+  if (ksplit > 1) {
+    // Split-K hand-off (conv_pipe.hip's scheme): each thread's raw partial accumulators go to
+    // slab[unit][slice][thread] with write-through sc1 stores; every wave drains them and the
+    // workgroup barrier orders that before one relaxed agent-scope ticket; the workgroup drawing
+    // ksplit - 1 sums every slice from the slab in slice order (sc1 loads, its own included:
+    // bit-identical whichever arrives last), resets the ticket and runs the epilogue below
+    constexpr int SC1 = 16, PER = NA * 16;  // floats per thread
+    i32x4 rs;
+    {
+      const unsigned long long a = (unsigned long long)(p.slab + (size_t)unit * ksplit * NT * PER);
+      rs = i32x4{(int)(unsigned)a, (int)(unsigned)(a >> 32), ksplit * NT * PER * 4, 0x00020000};
+    }
+    const int toff = tid * PER * 4;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        raw_buffer_store_v4(u32x4{__float_as_uint(acc[i][4 * g]), __float_as_uint(acc[i][4 * g + 1]),
+                                  __float_as_uint(acc[i][4 * g + 2]), __float_as_uint(acc[i][4 * g + 3])},
+                            rs, toff + (i * 4 + g) * 16, slice * NT * PER * 4, SC1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* last_flag = reinterpret_cast<unsigned*>(smem);  // (operand buffers: every read done)
+    if (tid == 0) *last_flag = __hip_atomic_fetch_add((gu32*)(p.cnt + unit), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*last_flag != (unsigned)(ksplit - 1)) return;  // workgroup-uniform
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: every slab load below is sc1
+    if (tid == 0) __hip_atomic_store((gu32*)(p.cnt + unit), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 v = __builtin_bit_cast(f32x4, raw_buffer_load_v4(rs, toff + (i * 4 + g) * 16, 0, SC1));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][4 * g + e] = v[e];
+      }
+#pragma unroll 1
+    for (int sl = 1; sl < ksplit; ++sl) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = __builtin_bit_cast(f32x4, raw_buffer_load_v4(rs, toff + (i * 4 + g) * 16, sl * NT * PER * 4, SC1));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][4 * g + e] += v[e];
+        }
+    }
   }
 
   // ---- epilogue (as dcn_gemm)
@@ -1070,11 +1127,28 @@ static void launch64(const DcnParams& p, hipStream_t s) {
   constexpr int lds = lds_bytes2<BN, PX>();
   (void)ensure_lds<dcn_gemm64<T, BN, PX>>(lds);
   const long M = (long)p.B * p.H * p.W;
-  const dim3 grid((unsigned)((M + PX - 1) / PX * (p.N / BN)));
+  const dim3 grid((unsigned)((M + PX - 1) / PX * (p.N / BN) * (p.ksplit > 1 ? p.ksplit : 1)));
   hipLaunchKernelGGL((dcn_gemm64<T, BN, PX>), grid, dim3(NT), lds, s, p);
 }
 
 }  // namespace dcn
+
+void dcn64_tile(const DcnParams& p, int dcn64_mode, int* bn, int* px) {
+  // launch_dcn_gemm's choice for dcn_gemm64 (modes 1 / 2 and the fallback of 3 / 4)
+  const long M = (long)p.B * p.H * p.W;
+  const bool wide = p.N % 128 == 0;
+  const long tiles128 = (M + 127) / 128 * (p.N / 128);
+  *bn = wide ? 128 : 64;
+  *px = !wide || dcn64_mode == 2 || tiles128 < 1024 ? 64 : 128;
+}
+
+long dcn_split_floats(const DcnParams& p, int dcn64_mode, int ksplit) {
+  int bn, px;
+  dcn64_tile(p, dcn64_mode, &bn, &px);
+  const long M = (long)p.B * p.H * p.W;
+  const int na = bn / 32 / (4 / (px / 32));
+  return (M + px - 1) / px * (p.N / bn) * ksplit * dcn::NT * na * 16;
+}
 
 bool dcn_gemm_supported(long M, int C, int N, int ldx, int om_ldc, int out_ldc, int Kpad) {
   // buffer offsets are 32-bit: the input and weight tensors stay below the out-of-range marker
@@ -1099,6 +1173,10 @@ int launch_dcn_gemm(const DcnParams& p, int dtype, int dcn64_mode, int cu_count,
   dim3 grid((unsigned)((M + dcn::BMP - 1) / dcn::BMP * (p.N / (wide ? 128 : 64))));
   if (dtype != F16 && dtype != BF16) {
     set_error("dcn_gemm: fp16/bf16 only");
+    return 1;
+  }
+  if (p.ksplit > 1 && (!p.slab || !p.cnt || p.ksplit > 9 || p.C % 64 || !dcn64_mode || dcn64_mode >= 3)) {
+    set_error("dcn_gemm: split-K needs dcn_gemm64 (modes 1 / 2), a slab, tickets and <= 9 slices");
     return 1;
   }
   if ((dcn64_mode == 3 || dcn64_mode == 4) && dcn_win_supported(p)) {  // LDS window (C == N == 64; mode 4: diagnostics only)

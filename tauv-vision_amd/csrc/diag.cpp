@@ -50,7 +50,7 @@ namespace tv {
 int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int om_ldc, const float* weight,
                   const float* bias, int N, int act, int dtype, int variant, void* out, hipStream_t s) {
   if (!x || !om || !weight || !bias || !out || B < 1 || H < 1 || W < 1 || C < 1 || N < 1 || om_ldc < 27 ||
-      variant < 0 || variant > 5 || dtype < F32 || dtype > BF16 || act < 0 || act > 2) {
+      variant < 0 || variant > 8 || dtype < F32 || dtype > BF16 || act < 0 || act > 2) {
     set_error("diag_dcn_conv: bad argument");
     return TV_EINVAL;
   }
@@ -70,7 +70,7 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
       for (int t = 0; t < 9; ++t) put(hw, (size_t)n * Kpad + (size_t)t * C + c, weight[((size_t)n * C + c) * 9 + t], dtype);
   std::vector<float> hb(Npad, 0.f);
   std::memcpy(hb.data(), bias, N * sizeof(float));
-  DevBuf dw, db, dcols, dpar, dzero;
+  DevBuf dw, db, dcols, dpar, dzero, dslab, dcnt;
   TV_HIP(hipMalloc(&dw.p, hw.size()));
   TV_HIP(hipMemcpy(dw.p, hw.data(), hw.size(), hipMemcpyHostToDevice));
   TV_HIP(hipMalloc(&db.p, hb.size() * 4));
@@ -104,7 +104,18 @@ int diag_dcn_conv(const void* x, const void* om, int B, int H, int W, int C, int
     int dev = 0, cus = 0;
     TV_HIP(hipGetDevice(&dev));
     TV_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    rc = launch_dcn_gemm(q, dtype, variant == 4 ? 3 : variant, cus, s);
+    int mode = variant == 4 ? 3 : variant;
+    if (variant >= 6) {  // dcn_gemm64 on 64-pixel tiles, split-K over 3 / 4 / 9 tap ranges
+      mode = 2;
+      q.ksplit = variant == 6 ? 3 : variant == 7 ? 4 : 9;
+      const long units = ((long)B * H * W + 63) / 64 * (N / (N % 128 == 0 ? 128 : 64));
+      TV_HIP(hipMalloc(&dslab.p, (size_t)dcn_split_floats(q, mode, q.ksplit) * sizeof(float)));
+      TV_HIP(hipMalloc(&dcnt.p, (size_t)units * sizeof(unsigned)));
+      TV_HIP(hipMemset(dcnt.p, 0, (size_t)units * sizeof(unsigned)));
+      q.slab = (float*)dslab.p;
+      q.cnt = (unsigned*)dcnt.p;
+    }
+    rc = launch_dcn_gemm(q, dtype, mode, cus, s);
   } else {
     const size_t cols_bytes = (size_t)B * H * W * K * esz;
     TV_HIP(hipMalloc(&dcols.p, cols_bytes));

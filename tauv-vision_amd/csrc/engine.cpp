@@ -334,6 +334,7 @@ int Engine::create(const tv_model_desc& d, const tv_weight_view* w, int n, int d
     else if (k == "TV_C1X1") c1x1_mode = std::max(0, std::min(2, v));
     else if (k == "TV_LATGROUP_B") lat_group_max_b = std::max(1, v);
     else if (k == "TV_DCN64") dcn64_mode = v;
+    else if (k == "TV_DCN_SPLIT") dcn_split_max = std::max(0, std::min(9, v));
     else if (k == "TV_CONVT") convt_mode = v;
     else if (k == "TV_CONV3S2") s2_mode = v;
     else if (k == "TV_CONV3_MINPIX") conv3_min_pix = v;
@@ -453,6 +454,8 @@ Engine::~Engine() {
     for (hipEvent_t ev : kv.second->gev) (void)hipEventDestroy(ev);
     if (kv.second->pslab) (void)hipFree(kv.second->pslab);
     if (kv.second->pcnt) (void)hipFree(kv.second->pcnt);
+    if (kv.second->dslab) (void)hipFree(kv.second->dslab);
+    if (kv.second->dcnt) (void)hipFree(kv.second->dcnt);
     if (kv.second->cnt) (void)hipFree(kv.second->cnt);
     delete kv.second;
   }
@@ -846,6 +849,34 @@ int Engine::make_workspace(int B, Workspace* ws) {
     ws->dcn_skip[i] = 1;
     ws->use_pipe[i + 1] = 0;
   }
+  // dcn_gemm64 split-K: a layer whose (pixel, channel) tiles fill at most half the CUs (DLA-34 at
+  // B=1: a 30x40 256-channel layer is 38 tiles of 36 k-steps, each k-step a chain of corner gathers)
+  // runs ksplit workgroups per tile over tap ranges; their fp32 partials meet in dslab
+  if (dcn_split_max >= 2 && (dcn64_mode == 1 || dcn64_mode == 2)) {
+    long slab_floats = 0, tickets = 0;
+    for (size_t i = 0; i < plan.ops.size(); ++i) {
+      DcnParams& q = ws->dcn[i];
+      if (!q.x || q.C % 64) continue;
+      int bn, px;
+      dcn64_tile(q, dcn64_mode, &bn, &px);
+      const long units = ((long)q.B * q.H * q.W + px - 1) / px * (q.N / bn);
+      const int ks = (int)std::min<long>(dcn_split_max, cu_count / std::max(1L, units));
+      if (ks < 2) continue;
+      q.ksplit = ks;
+      slab_floats = std::max(slab_floats, dcn_split_floats(q, dcn64_mode, ks));
+      tickets = std::max(tickets, units);
+    }
+    if (tickets) {
+      TV_HIP(hipMalloc((void**)&ws->dslab, (size_t)slab_floats * sizeof(float)));
+      TV_HIP(hipMalloc((void**)&ws->dcnt, (size_t)tickets * sizeof(unsigned)));
+      TV_HIP(hipMemset(ws->dcnt, 0, (size_t)tickets * sizeof(unsigned)));
+      for (size_t i = 0; i < plan.ops.size(); ++i)
+        if (ws->dcn[i].ksplit > 1) {
+          ws->dcn[i].slab = ws->dslab;
+          ws->dcn[i].cnt = ws->dcnt;
+        }
+    }
+  }
   // stacked 3x3 heads on conv3x3 + block-diagonal 1x1 heads -> one launch (EPI 1)
   ws->head_fused.assign(plan.ops.size(), 0);
   ws->head_skip.assign(plan.ops.size(), 0);
@@ -1223,6 +1254,8 @@ int Engine::get_workspace(int B, hipStream_t stream, Workspace** out) {
     for (hipEvent_t ev : ws->gev) (void)hipEventDestroy(ev);
     if (ws->pslab) (void)hipFree(ws->pslab);
     if (ws->pcnt) (void)hipFree(ws->pcnt);
+    if (ws->dslab) (void)hipFree(ws->dslab);
+    if (ws->dcnt) (void)hipFree(ws->dcnt);
     if (ws->cnt) (void)hipFree(ws->cnt);
     delete ws;
     return rc;
@@ -1244,6 +1277,8 @@ int Engine::trim() {
     for (hipEvent_t ev : kv.second->gev) (void)hipEventDestroy(ev);
     if (kv.second->pslab) (void)hipFree(kv.second->pslab);
     if (kv.second->pcnt) (void)hipFree(kv.second->pcnt);
+    if (kv.second->dslab) (void)hipFree(kv.second->dslab);
+    if (kv.second->dcnt) (void)hipFree(kv.second->dcnt);
     if (kv.second->cnt) (void)hipFree(kv.second->cnt);
     delete kv.second;
   }
@@ -1605,6 +1640,7 @@ const char* Engine::op_kernel(int B, size_t i) {
           const long tiles128 = ((long)d.B * d.H * d.W + 127) / 128 * (d.N / 128);
           const int px = !wide || dcn64_mode == 2 || tiles128 < 1024 ? 64 : 128;
           name = std::string("tv::dcn::dcn_gemm64<") + t + (wide ? ", 128, " : ", 64, ") + std::to_string(px) + ">";
+          if (d.ksplit > 1) name += " split-K " + std::to_string(d.ksplit);
         } else {
           name = std::string("tv::dcn::dcn_gemm<") + t + (wide ? ", 128>" : ", 64>");
         }

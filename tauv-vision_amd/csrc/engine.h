@@ -63,6 +63,8 @@ struct Workspace {
   unsigned* cnt = nullptr;          // conv_lat split-K tickets, one per tile and slot, zeroed per forward
   float* pslab = nullptr;           // conv_pipe split-K partial tiles (one layer at a time)
   unsigned* pcnt = nullptr;         // conv_pipe split-K tickets, one per tile (reset by the last slice)
+  float* dslab = nullptr;           // dcn_gemm64 split-K partial accumulators (one layer at a time)
+  unsigned* dcnt = nullptr;         // dcn_gemm64 split-K tickets, one per tile (reset by the last slice)
   std::vector<int> level;           // per op: dependency level (the arena's time; plan order when not grouping)
   std::vector<int> order;           // the ops in execution order: by level, then plan order
   std::vector<std::vector<int>> groups;  // the schedule: conv_lat layers of one level in one launch, others alone
@@ -105,6 +107,10 @@ struct Engine {
                                // bit-equal, measured 194 vs 187 us per 120x160 layer, so not the default; 5 dcn_gemm64d:
                                // the corner gathers two k-steps ahead)
   int lat_units = -1;          // threshold in work units (env TV_LAT_UNITS; -1 = cu_count)
+  int dcn_split_max = 4;       // dcn_gemm64 split-K over tap ranges for layers whose tiles fill <= half the CUs
+                               // (the latency path: DLA-34 at B=1), at most this many slices (knob TV_DCN_SPLIT, <2 off;
+                               // B=1 DLA-34 1.263 -> 1.149 ms; 6 / 9 slices equal, counting 2 / 4 resident
+                               // workgroups per CU as slots slower: 1.186 / 1.225 ms)
   int c1x1_mode = 1;           // stride-1 1x1 convs on the streaming kernel (knob TV_C1X1; 2 = N <= 128 only)
   int lat_group = 1;           // independent conv_lat layers of one dependency level in one launch (knob TV_LATGROUP)
   int lat_group_max_b = 8;     // ... on workspaces of at most this many frames (knob TV_LATGROUP_B)

@@ -37,7 +37,7 @@ TOL = {"fp32": 2e-5, "fp16": 4e-3, "bf16": 3e-2}
 def variants(precision, C, N=None):
     if precision == "fp32":
         return [3]
-    v = [0, 1, 2, 3, 5] if C % 64 == 0 else [0, 3]
+    v = [0, 1, 2, 3, 5, 6, 7, 8] if C % 64 == 0 else [0, 3]
     return v + [4] if C == 64 and N == 64 else v
 
 
@@ -195,3 +195,24 @@ def test_dcn_deep_prefetch_bit_equal(precision, shape):
                    torch.randn(B, 9, H, W, generator=g) * 2.0), precision)
     got = dcn_gpu(x, om, w, b, 1, precision, 5)
     assert torch.equal(got, dcn_gpu(x, om, w, b, 1, precision, 2)), "dcn_gemm64d must equal dcn_gemm64 bit for bit"
+
+
+@pytest.mark.parametrize("precision", ["fp16", "bf16"])
+@pytest.mark.parametrize("shape", [(1, 256, 30, 40, 256), (1, 64, 60, 80, 64), (2, 128, 15, 21, 128), (1, 256, 5, 7, 128)])
+def test_dcn_split_k(precision, shape):
+    """dcn_gemm64 split-K over tap ranges (variants 6 / 7 / 8: 3 / 4 / 9 slices of the 9 taps — the
+    engine's form for DLA-34's small-batch DeformConvs): each slice's fp32 partial accumulators go
+    through the slab and the last-arriving workgroup sums them in slice order, so the result is
+    the unsplit kernel's up to the fp32 summation order (within the output rounding) and
+    bit-identical run to run; the tickets reset themselves (the repeats reuse fresh slabs here, the
+    engine's workspace reuse is covered by the DLA-34 B=1 tests)."""
+    B, C, H, W, N = shape
+    x, w, b, g = inputs(B, C, H, W, N, precision, 29)
+    om = rnd(om_of(torch.randn(B, 9, H, W, generator=g) * 1.5, torch.randn(B, 9, H, W, generator=g) * 1.5,
+                   torch.randn(B, 9, H, W, generator=g) * 2.0), precision)
+    ref = dcn_gpu(x, om, w, b, 1, precision, 2)
+    for v in (6, 7, 8):
+        got = dcn_gpu(x, om, w, b, 1, precision, v)
+        assert torch.isfinite(got).all(), f"variant {v}"
+        assert torch.equal(got, dcn_gpu(x, om, w, b, 1, precision, v)), f"variant {v}: not deterministic"
+        assert_close(got, ref, ULP[precision], f"variant {v} vs unsplit")
